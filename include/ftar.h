@@ -1,0 +1,180 @@
+/*
+ * ftar.h -- C ABI of the MI355X-native fault-tolerant Allreduce (libftar.so).
+ *
+ * This is the drop-in boundary for the hot path of LucaMica02/Fault-Tolerant:
+ * the two fault-tolerant Allreduce schedules (recursive doubling, Rabenseifner)
+ * and the local reduction they call after every exchange.  Every entry point is
+ * plain C: pointers, sizes and enums, no HIP or torch types in the signatures.
+ * Device buffers are passed as `void *` (hipMalloc'd or torch tensor storage).
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   ftar_recursive_doubling      <- recursive_doubling()        src/rd/header.h:29
+ *   ftar_allreduce_rabenseifner  <- allreduce_rabenseifner()    src/raben/header.h:14-15
+ *   ftar_reduce_local            <- MPI_Reduce_local(in, inout) call sites
+ *                                   src/rd/util.c:32, src/rd/recursive_doubling.c:44,48,
+ *                                   src/raben/rabenseifner.c:86,117,234-236
+ *   ftar_init / ftar_finalize    <- MPI_Init + MPI_Comm_dup(MPI_COMM_WORLD)
+ *                                   src/raben/rabenseifner.c:441-454, src/rd/recursive_doubling.c:100
+ *   ftar_abort                   <- MPI_Abort   (src/rd/util.c:75, src/raben/errhandler.c:38,211)
+ *   ftar_barrier                 <- MPI_Barrier (src/rd/recursive_doubling.c:134)
+ *   ULFM MPIX_Comm_agree / failure_ack / failure_get_acked / shrink and the
+ *   group re-ordering in the error handlers are internal to the library
+ *   (src/rd/errhandler.c, src/raben/errhandler.c); they surface only as the
+ *   comm being re-targeted (rank/size queries change) after a recovery.
+ */
+#ifndef FTAR_H
+#define FTAR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes: the MPI error classes the reference relies on ---------- */
+#define FTAR_SUCCESS         0   /* MPI_SUCCESS */
+#define FTAR_ERR_ARG         13  /* MPI_ERR_ARG      (raben/rabenseifner.c:18-20) */
+#define FTAR_ERR_UNKNOWN     14  /* MPI_ERR_UNKNOWN  (raben/util.c:40-43) */
+#define FTAR_ERR_OTHER       16  /* MPI_ERR_OTHER    (rd/util.c:75) */
+#define FTAR_ERR_PROC_FAILED 75  /* MPIX_ERR_PROC_FAILED, hard-coded 75 in rd/recursive_doubling.c:56 */
+#define FTAR_ERR_DEVICE      101 /* a HIP call failed */
+#define FTAR_ERR_NOMEM       102 /* allocation failed */
+#define FTAR_ERR_STATE       103 /* library not initialised / job aborted */
+
+/* ---- element types and reduction ops ------------------------------------- */
+typedef enum {
+    FTAR_INT32 = 0,   /* MPI_INT (the only type the reference drivers use) */
+    FTAR_FLOAT32 = 1, /* north-star type */
+    FTAR_INT64 = 2,
+    FTAR_FLOAT64 = 3
+} ftar_dtype;
+
+typedef enum {
+    FTAR_SUM = 0,  /* MPI_SUM (the only op the reference drivers use) */
+    FTAR_PROD = 1,
+    FTAR_MAX = 2,
+    FTAR_MIN = 3
+} ftar_op;
+
+/* ---- deterministic fault injection --------------------------------------
+ * A kill names the victim (original world rank) and the place in the schedule
+ * where it dies.  Phases follow the reference's control flow:
+ *   FTAR_PH_PRE   RD reduce_pow2 (rd/util.c:3-34) / Raben pre-step (raben/rabenseifner.c:65-139)
+ *   FTAR_PH_LOOP  RD distance loop (rd/recursive_doubling.c:21-71) / Raben reduce-scatter
+ *                 loop (raben/rabenseifner.c:170-284); `step` = loop iteration (reference `step`)
+ *   FTAR_PH_AG    Raben allgather loop (raben/rabenseifner.c:299-355); `step` = the reference's
+ *                 `step` variable, i.e. steps-1 for the first allgather exchange
+ *   FTAR_PH_POST  after the fault-tolerant region (ERRORS_ARE_FATAL barrier, fan-out / post-step)
+ * Points inside a step:
+ *   FTAR_PT_BEFORE   dies before its exchange of that step (partner's receive fails)
+ *   FTAR_PT_AFTER    exchange done, dies before its local reduce / before arriving at the barrier
+ *   FTAR_PT_BARRIER  completes the step, waits until every peer arrived, then dies (no peer ever
+ *                    touches its memory while it dies)
+ */
+#define FTAR_PH_PRE  0
+#define FTAR_PH_LOOP 1
+#define FTAR_PH_AG   2
+#define FTAR_PH_POST 3
+
+#define FTAR_PT_BEFORE  0
+#define FTAR_PT_AFTER   1
+#define FTAR_PT_BARRIER 2
+
+typedef struct {
+    int rank;  /* original world rank of the victim */
+    int phase; /* FTAR_PH_* */
+    int step;  /* step inside the phase */
+    int point; /* FTAR_PT_* */
+} ftar_kill;
+
+#define FTAR_MAX_RANKS 63 /* the agree decision word holds one bit per rank + a decided bit */
+#define FTAR_MAX_KILLS 16
+
+/* ---- communicator -------------------------------------------------------- */
+typedef struct ftar_comm ftar_comm;
+
+/* Bootstrap from the environment: FTAR_JOB/FTAR_RANK/FTAR_SIZE/FTAR_DEVICE (set by
+ * the `ftrun` launcher) or torchrun's RANK/WORLD_SIZE/LOCAL_RANK/MASTER_PORT.  Also
+ * reads FTAR_KILL="rank:phase:step:point[,...]" for deterministic fault injection. */
+int ftar_init(ftar_comm **comm);
+/* Explicit bootstrap: `job` names the shared control block (all ranks pass the same),
+ * `device` is the HIP device ordinal this rank drives. */
+int ftar_init_rank(ftar_comm **comm, const char *job, int rank, int size, int device);
+int ftar_finalize(ftar_comm *comm);
+
+int ftar_comm_rank(const ftar_comm *comm, int *rank);       /* rank in the current (maybe shrunk) comm */
+int ftar_comm_size(const ftar_comm *comm, int *size);       /* size of the current comm */
+int ftar_world_rank(const ftar_comm *comm, int *rank);      /* original rank (Data.original_rank) */
+int ftar_world_size(const ftar_comm *comm, int *size);      /* original size (Data.original_size) */
+int ftar_comm_device(const ftar_comm *comm, int *device);   /* HIP device ordinal */
+
+int ftar_barrier(ftar_comm *comm);                 /* ERRORS_ARE_FATAL barrier over the survivors */
+void ftar_abort(ftar_comm *comm, int errorcode);   /* MPI_Abort: kills the whole job, never returns */
+
+/* Deterministic fault injection (in addition to FTAR_KILL). */
+int ftar_set_kills(ftar_comm *comm, const ftar_kill *kills, int nkills);
+
+/* ---- the hot path ---------------------------------------------------------
+ * Device-resident, blocking (return when the result is in the output buffer).
+ * `stream` ordering: the call first waits for all work queued on the stream set
+ * with ftar_comm_set_stream (default: the null stream) to finish.
+ */
+
+/* Fault-tolerant Rabenseifner Allreduce (raben/rabenseifner.c:3-395).
+ * sbuf is never written (the reference writes through its const sbuf; the build keeps
+ * a private device shadow instead).  On recovery the comm is re-targeted in place:
+ * ftar_comm_rank/size change exactly as the reference's *comm replacement does. */
+int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count,
+                                ftar_dtype dtype, ftar_op op, ftar_comm *comm);
+
+/* Fault-tolerant recursive doubling (rd/recursive_doubling.c:6-90).  The reference
+ * clobbers src as its accumulator; the build leaves src untouched.  The Data struct of
+ * the reference (rd/header.h:16-26) lives inside the comm. */
+int ftar_recursive_doubling(const void *src, void *dst, size_t count,
+                            ftar_dtype dtype, ftar_op op, ftar_comm *comm);
+
+/* Same schedules on host buffers: pinned H2D, device-resident allreduce, D2H. */
+int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
+                                     ftar_dtype dtype, ftar_op op, ftar_comm *comm);
+int ftar_recursive_doubling_host(const void *src, void *dst, size_t count,
+                                 ftar_dtype dtype, ftar_op op, ftar_comm *comm);
+
+/* MPI_Reduce_local(in, inout, count, dtype, op) on the device:
+ * inout[i] = in[i] (op) inout[i] with the reference's operand roles.
+ * `stream` is a hipStream_t (NULL = null stream); the call is asynchronous. */
+int ftar_reduce_local(const void *in, void *inout, size_t count,
+                      ftar_dtype dtype, ftar_op op, void *stream);
+
+/* Which implementation of the local-reduce kernel ftar_reduce_local launches:
+ * 0 = register-streaming float4 kernel (default), 1 = LDS-DMA staged kernel. */
+int ftar_set_reduce_variant(int variant);
+
+/* Stream the comm orders its work after (hipStream_t, NULL = null stream). */
+int ftar_comm_set_stream(ftar_comm *comm, void *stream);
+
+/* ---- statistics of the last allreduce call on this rank ----------------- */
+typedef struct {
+    int    steps;            /* exchange steps executed (pre/loop/allgather/post) */
+    int    recoveries;       /* error-handler invocations that recovered */
+    int    comm_size_after;  /* comm size after the call */
+    double wall_s;           /* host wall time of the call */
+    double kernel_ms;        /* sum of device time of all kernels of the call (profiling on) */
+    double step0_kernel_ms;  /* device time of the dominant kernel (RD step / Raben step 0) */
+    double link_bytes;       /* bytes this rank pulled over the fabric (algorithmic) */
+    double hbm_bytes;        /* algorithmic HBM bytes of this rank's kernels */
+    int    kernels;          /* kernels launched */
+} ftar_stats;
+
+int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);
+/* Record hipEvents around every kernel of the schedules (for bench.py's roofline). */
+int ftar_set_profiling(ftar_comm *comm, int on);
+
+/* Version string of the library build. */
+const char *ftar_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FTAR_H */
