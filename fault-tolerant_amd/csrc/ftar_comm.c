@@ -1,0 +1,431 @@
+/*
+ * ftar_comm.c -- communicator bootstrap, workspace exchange, synchronisation and the
+ * small C-ABI entry points (rank queries, barrier, abort, local reduce, statistics).
+ *
+ * Bootstrap replaces MPI_Init + MPI_Comm_dup(MPI_COMM_WORLD)
+ * (raben/rabenseifner.c:439-454, rd/recursive_doubling.c:100-103).
+ */
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
+#include "ftar_internal.h"
+
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#define WS_ALIGN (2u << 20)
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+size_t ftar_esize(int dtype)
+{
+    switch (dtype) {
+    case FTAR_INT32:
+    case FTAR_FLOAT32: return 4;
+    case FTAR_INT64:
+    case FTAR_FLOAT64: return 8;
+    default: return 0;
+    }
+}
+
+int ftar_hibit(int value, int start) /* raben/util.c:22-37 */
+{
+    unsigned int mask = (unsigned int)value & ((1u << start) - 1u);
+    if (mask == 0) return -1;
+    return (int)(8 * sizeof(int) - 1) - __builtin_clz(mask);
+}
+
+int ftar_floor_pow2(int n) /* (int)pow(2, floor(log2(n))), rd/util.c:5 */
+{
+    int p = 1;
+    while (p * 2 <= n) p *= 2;
+    return p;
+}
+
+int ftar_my_comm_rank(const ftar_comm *c) { return ftar_comm_rank_of(c, c->wrank); }
+
+int ftar_comm_rank_of(const ftar_comm *c, int w)
+{
+    for (int i = 0; i < c->size; i++)
+        if (c->order[i] == w) return i;
+    return -1;
+}
+
+static void recompute_members(ftar_comm *c)
+{
+    c->members = 0;
+    for (int i = 0; i < c->size; i++) c->members |= 1ull << c->order[i];
+}
+
+/* ---- fault injection ---------------------------------------------------- */
+
+static int parse_kills(const char *s, ftar_kill *out, int max)
+{
+    int n = 0;
+    while (s && *s && n < max) {
+        ftar_kill k;
+        int used = 0;
+        if (sscanf(s, "%d:%d:%d:%d%n", &k.rank, &k.phase, &k.step, &k.point, &used) != 4) break;
+        out[n++] = k;
+        s += used;
+        while (*s == ',' || *s == ' ' || *s == ';') s++;
+    }
+    return n;
+}
+
+void ftar_maybe_die(ftar_comm *c, int phase, int step, int point)
+{
+    for (int i = 0; i < c->nkills; i++) {
+        const ftar_kill *k = &c->kills[i];
+        if (k->rank != c->wrank || k->phase != phase || k->step != step || k->point != point) continue;
+        if (point == FTAR_PT_BARRIER) /* let every peer finish the step first */
+            ftar_ctrl_wait_peers_arrived(&c->job, c->members, c->job.seq + 1);
+        if (c->verbose) fprintf(stderr, "ftar: rank %d dies at phase %d step %d point %d\n", c->wrank, phase, step, point);
+        fflush(stdout);
+        fflush(stderr);
+        raise(SIGKILL);
+    }
+}
+
+int ftar_set_kills(ftar_comm *c, const ftar_kill *kills, int nkills)
+{
+    if (!c || nkills < 0 || nkills > FTAR_MAX_KILLS) return FTAR_ERR_ARG;
+    memcpy(c->kills, kills, sizeof(ftar_kill) * (size_t)nkills);
+    c->nkills = nkills;
+    return FTAR_SUCCESS;
+}
+
+/* ---- bootstrap ------------------------------------------------------------ */
+
+int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int device)
+{
+    *out = NULL;
+    if (!job || rank < 0 || size < 1 || rank >= size || size > FTAR_MAX_RANKS) return FTAR_ERR_ARG;
+    ftar_comm *c = (ftar_comm *)calloc(1, sizeof(ftar_comm));
+    if (!c) return FTAR_ERR_NOMEM;
+    c->wrank = rank;
+    c->wsize = size;
+    c->device = device;
+    c->verbose = getenv("FTAR_VERBOSE") ? atoi(getenv("FTAR_VERBOSE")) : 0;
+    int create = getenv("FTAR_LAUNCHER") == NULL;
+    int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
+    if (rc) {
+        free(c);
+        return rc;
+    }
+    rc = fdev_open(device, &c->dev);
+    if (rc) {
+        fprintf(stderr, "ftar: rank %d: device %d: %s\n", rank, device, fdev_last_error());
+        ftar_ctrl_detach(&c->job);
+        free(c);
+        return rc;
+    }
+    rc = ftar_ctrl_join(&c->job, device);
+    if (rc) {
+        fdev_close(c->dev);
+        ftar_ctrl_detach(&c->job);
+        free(c);
+        return rc;
+    }
+    c->size = size;
+    for (int i = 0; i < size; i++) c->order[i] = i;
+    recompute_members(c);
+    c->acked = 0;
+    const char *ks = getenv("FTAR_KILL");
+    if (ks) c->nkills = parse_kills(ks, c->kills, FTAR_MAX_KILLS);
+    /* every rank has mapped the control block once this round completes */
+    ftar_sync_fatal(c);
+    if (rank == 0) shm_unlink(job);
+    *out = c;
+    return FTAR_SUCCESS;
+}
+
+int ftar_init(ftar_comm **out)
+{
+    char name[128];
+    int rank, size, device = -1;
+    const char *e;
+    if ((e = getenv("FTAR_JOB")) && getenv("FTAR_RANK") && getenv("FTAR_SIZE")) {
+        snprintf(name, sizeof(name), "%s", e);
+        rank = atoi(getenv("FTAR_RANK"));
+        size = atoi(getenv("FTAR_SIZE"));
+    } else if (getenv("RANK") && getenv("WORLD_SIZE")) { /* torchrun */
+        rank = atoi(getenv("RANK"));
+        size = atoi(getenv("WORLD_SIZE"));
+        const char *port = getenv("MASTER_PORT");
+        snprintf(name, sizeof(name), "/ftar-%s-%d", port ? port : "0", (int)getppid());
+        if (getenv("LOCAL_RANK")) device = atoi(getenv("LOCAL_RANK"));
+    } else {
+        rank = 0;
+        size = 1;
+        snprintf(name, sizeof(name), "/ftar-solo-%d", (int)getpid());
+    }
+    if ((e = getenv("FTAR_DEVICE"))) device = atoi(e);
+    int ndev = 0;
+    int rc = fdev_device_count(&ndev);
+    if (rc || ndev < 1) {
+        fprintf(stderr, "ftar: rank %d: no HIP device visible (%s)\n", rank, fdev_last_error());
+        return FTAR_ERR_DEVICE;
+    }
+    if (device < 0) device = rank;
+    device %= ndev;
+    return ftar_init_rank(out, name, rank, size, device);
+}
+
+static void release_peers(ftar_comm *c)
+{
+    for (int w = 0; w < c->wsize; w++)
+        for (int b = 0; b < FTAR_NBUF; b++)
+            if (c->peer[w][b]) {
+                fdev_unimport(c->dev, c->peer[w][b]);
+                c->peer[w][b] = NULL;
+            }
+}
+
+int ftar_finalize(ftar_comm *c)
+{
+    if (!c) return FTAR_ERR_ARG;
+    ftar_sync_fatal(c);
+    release_peers(c);
+    ftar_sync_fatal(c); /* nobody maps our workspace any more */
+    for (int b = 0; b < FTAR_NBUF; b++) fdev_free(c->dev, c->ws[b]);
+    fdev_free(c->dev, c->hsend);
+    fdev_free(c->dev, c->hrecv);
+    ftar_ctrl_leave(&c->job);
+    fdev_close(c->dev);
+    ftar_ctrl_detach(&c->job);
+    free(c);
+    return FTAR_SUCCESS;
+}
+
+int ftar_comm_rank(const ftar_comm *c, int *r)
+{
+    if (!c || !r) return FTAR_ERR_ARG;
+    *r = ftar_my_comm_rank(c);
+    return FTAR_SUCCESS;
+}
+int ftar_comm_size(const ftar_comm *c, int *s)
+{
+    if (!c || !s) return FTAR_ERR_ARG;
+    *s = c->size;
+    return FTAR_SUCCESS;
+}
+int ftar_world_rank(const ftar_comm *c, int *r)
+{
+    if (!c || !r) return FTAR_ERR_ARG;
+    *r = c->wrank;
+    return FTAR_SUCCESS;
+}
+int ftar_world_size(const ftar_comm *c, int *s)
+{
+    if (!c || !s) return FTAR_ERR_ARG;
+    *s = c->wsize;
+    return FTAR_SUCCESS;
+}
+int ftar_comm_device(const ftar_comm *c, int *d)
+{
+    if (!c || !d) return FTAR_ERR_ARG;
+    *d = c->device;
+    return FTAR_SUCCESS;
+}
+
+int ftar_comm_set_stream(ftar_comm *c, void *stream)
+{
+    if (!c) return FTAR_ERR_ARG;
+    c->user_stream = stream;
+    return FTAR_SUCCESS;
+}
+
+void ftar_abort(ftar_comm *c, int code) { ftar_ctrl_abort(&c->job, code); }
+
+int ftar_barrier(ftar_comm *c)
+{
+    if (!c) return FTAR_ERR_ARG;
+    ftar_sync_fatal(c);
+    return FTAR_SUCCESS;
+}
+
+/* ---- synchronisation ------------------------------------------------------ */
+
+uint64_t ftar_sync(ftar_comm *c)
+{
+    uint64_t next = c->job.seq + 1;
+    atomic_store_explicit(&c->job.shm->slot[c->wrank].pubv[next % 2], (next << 16) | ((uint64_t)c->pubval & 0xffff),
+                          memory_order_release);
+    uint64_t snap = ftar_ctrl_agree(&c->job, c->members);
+    return snap & ~c->acked;
+}
+
+void ftar_sync_fatal(ftar_comm *c)
+{
+    uint64_t f = ftar_sync(c);
+    if (f) {
+        /* a failure outside the tolerant region: MPI_ERRORS_ARE_FATAL */
+        ftar_ctrl_abort(&c->job, FTAR_ERR_PROC_FAILED);
+    }
+}
+
+int64_t ftar_peer_pub(ftar_comm *c, int w)
+{
+    uint64_t s = c->job.seq;
+    uint64_t v = atomic_load_explicit(&c->job.shm->slot[w].pubv[s % 2], memory_order_acquire);
+    if ((v >> 16) != s) {
+        fprintf(stderr, "ftar: rank %d: stale publication of rank %d (round %llu, tag %llu)\n", c->wrank, w,
+                (unsigned long long)s, (unsigned long long)(v >> 16));
+        ftar_ctrl_abort(&c->job, FTAR_ERR_STATE);
+    }
+    return (int64_t)(v & 0xffff);
+}
+
+int ftar_is_dead(ftar_comm *c, int w) { return ftar_ctrl_is_dead(&c->job, w); }
+
+int ftar_drain(ftar_comm *c)
+{
+    int rc = fdev_sync(c->dev, ftar_ctrl_poll, &c->job);
+    if (rc) {
+        fprintf(stderr, "ftar: rank %d: device error: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    return rc;
+}
+
+int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    int rc = fdev_run(c->dev, dtype, op, segs, nseg, tag);
+    if (rc) {
+        fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    return rc;
+}
+
+void ftar_regroup(ftar_comm *c, int dead, int repl)
+{
+    int neworder[FTAR_MAX_RANKS];
+    int k = 0;
+    for (int i = 0; i < c->size; i++)
+        if (i != repl) neworder[k++] = c->order[i];
+    if (repl != dead) neworder[(dead < repl) ? dead : dead - 1] = c->order[repl];
+    memcpy(c->order, neworder, sizeof(int) * (size_t)k);
+    c->size = k;
+    recompute_members(c);
+}
+
+void ftar_shrink(ftar_comm *c, uint64_t failed)
+{
+    int k = 0;
+    for (int i = 0; i < c->size; i++)
+        if (!(failed & (1ull << c->order[i]))) c->order[k++] = c->order[i];
+    c->size = k;
+    recompute_members(c);
+}
+
+/* ---- workspace ------------------------------------------------------------ */
+
+void *ftar_buf(ftar_comm *c, int w, int b) { return (w == c->wrank) ? c->ws[b] : c->peer[w][b]; }
+
+int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
+{
+    if (bytes <= c->ws_bytes && c->ws[0]) return FTAR_SUCCESS;
+    size_t nb = (bytes + WS_ALIGN - 1) / WS_ALIGN * WS_ALIGN;
+    if (nb == 0) nb = WS_ALIGN;
+    ftar_sync_fatal(c); /* everybody is here */
+    release_peers(c);
+    ftar_sync_fatal(c); /* nobody maps the old buffers */
+    ftar_slot *me = &c->job.shm->slot[c->wrank];
+    for (int b = 0; b < FTAR_NBUF; b++) {
+        fdev_free(c->dev, c->ws[b]);
+        c->ws[b] = NULL;
+    }
+    for (int b = 0; b < FTAR_NBUF; b++) {
+        int rc = fdev_alloc_shared(c->dev, nb, &c->ws[b], me->handle[b]);
+        if (rc) {
+            fprintf(stderr, "ftar: rank %d: workspace allocation of %zu B failed: %s\n", c->wrank, nb,
+                    fdev_last_error());
+            ftar_ctrl_abort(&c->job, FTAR_ERR_NOMEM);
+        }
+    }
+    me->ws_bytes = nb;
+    atomic_fetch_add(&me->ws_gen, 1);
+    c->ws_bytes = nb;
+    ftar_sync_fatal(c); /* every handle is published */
+    for (int i = 0; i < c->size; i++) {
+        int w = c->order[i];
+        if (w == c->wrank) continue;
+        ftar_slot *s = &c->job.shm->slot[w];
+        for (int b = 0; b < FTAR_NBUF; b++) {
+            int rc = fdev_import(c->dev, s->handle[b], &c->peer[w][b]);
+            if (rc) {
+                fprintf(stderr, "ftar: rank %d: cannot map rank %d buffer %d: %s\n", c->wrank, w, b,
+                        fdev_last_error());
+                ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+            }
+        }
+        c->peer_bytes[w] = s->ws_bytes;
+    }
+    return FTAR_SUCCESS;
+}
+
+/* ---- statistics ----------------------------------------------------------- */
+
+static double g_t0;
+
+void ftar_stats_begin(ftar_comm *c)
+{
+    memset(&c->stats, 0, sizeof(c->stats));
+    fdev_counters_reset(c->dev);
+    g_t0 = now_s();
+}
+
+void ftar_stats_end(ftar_comm *c)
+{
+    fdev_counters k;
+    fdev_counters_get(c->dev, &k);
+    c->stats.wall_s = now_s() - g_t0;
+    c->stats.kernel_ms = k.ms[0] + k.ms[1] + k.ms[2] + k.ms[3];
+    c->stats.step0_kernel_ms = k.ms[FDEV_TAG_STEP0];
+    c->stats.link_bytes = k.link_bytes;
+    c->stats.hbm_bytes = k.hbm_bytes;
+    c->stats.kernels = k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3];
+    c->stats.comm_size_after = c->size;
+}
+
+int ftar_last_stats(const ftar_comm *c, ftar_stats *out)
+{
+    if (!c || !out) return FTAR_ERR_ARG;
+    *out = c->stats;
+    return FTAR_SUCCESS;
+}
+
+int ftar_set_profiling(ftar_comm *c, int on)
+{
+    if (!c) return FTAR_ERR_ARG;
+    c->profiling = on;
+    fdev_profiling(c->dev, on);
+    return FTAR_SUCCESS;
+}
+
+/* ---- local reduce --------------------------------------------------------- */
+
+int ftar_reduce_local(const void *in, void *inout, size_t count, ftar_dtype dtype, ftar_op op, void *stream)
+{
+    if (ftar_esize(dtype) == 0 || op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
+    if (count && (!in || !inout)) return FTAR_ERR_ARG;
+    int rc = fdev_reduce_local(in, inout, count, (int)dtype, (int)op, stream);
+    if (rc) fprintf(stderr, "ftar_reduce_local: %s\n", fdev_last_error());
+    return rc;
+}
+
+int ftar_set_reduce_variant(int v) { return fdev_set_reduce_variant(v) ? FTAR_ERR_ARG : FTAR_SUCCESS; }
+
+const char *ftar_version(void) { return "ftar-mi355x 0.1 (gfx950)"; }

@@ -1,0 +1,277 @@
+/*
+ * ftar_ctrl.c -- shared-memory control plane (see ftar_ctrl.h).
+ *
+ * Restates the ULFM services used by the reference (MPIX_Comm_agree,
+ * MPIX_Comm_failure_ack/get_acked, MPI_Barrier error return, MPI_Abort) for ranks
+ * that are processes on one node, without MPI:
+ *   - rd/recursive_doubling.c:51-53, raben/rabenseifner.c:258-260,330-332
+ *     (agree + barrier after every step) -> ftar_ctrl_agree
+ *   - rd/errhandler.c:21-40, raben/errhandler.c:15-31 (ack / get_acked / translate)
+ *     -> the sealed failure snapshot returned by ftar_ctrl_agree
+ *   - MPI_Abort (rd/util.c:75, raben/errhandler.c:38,211,322,378) -> ftar_ctrl_abort
+ */
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
+#include "ftar_ctrl.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static inline void cpu_relax(void)
+{
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+}
+
+static int map_segment(ftar_job *job, int fd)
+{
+    void *p = mmap(NULL, sizeof(ftar_shm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (p == MAP_FAILED) return FTAR_ERR_NOMEM;
+    job->shm = (ftar_shm *)p;
+    return FTAR_SUCCESS;
+}
+
+int ftar_ctrl_create(ftar_job *job, const char *name, int size)
+{
+    if (size < 1 || size > FTAR_MAX_RANKS) return FTAR_ERR_ARG;
+    memset(job, 0, sizeof(*job));
+    snprintf(job->name, sizeof(job->name), "%s", name);
+    int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0 && errno == EEXIST) { /* stale segment of a crashed job with the same name */
+        shm_unlink(name);
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    }
+    if (fd < 0) return FTAR_ERR_STATE;
+    if (ftruncate(fd, (off_t)sizeof(ftar_shm)) != 0) {
+        close(fd);
+        return FTAR_ERR_NOMEM;
+    }
+    int rc = map_segment(job, fd);
+    close(fd);
+    if (rc) return rc;
+    memset(job->shm, 0, sizeof(ftar_shm));
+    job->shm->magic = FTAR_SHM_MAGIC;
+    job->shm->version = FTAR_SHM_VERSION;
+    job->shm->size = size;
+    atomic_store_explicit(&job->shm->ready, 1, memory_order_release);
+    job->size = size;
+    job->rank = -1;
+    job->owner = 1;
+    return FTAR_SUCCESS;
+}
+
+int ftar_ctrl_attach(ftar_job *job, const char *name, int rank, int size, int create_if_rank0)
+{
+    if (rank < 0 || rank >= size || size > FTAR_MAX_RANKS) return FTAR_ERR_ARG;
+    if (create_if_rank0 && rank == 0) {
+        int rc = ftar_ctrl_create(job, name, size);
+        if (rc) return rc;
+        job->rank = 0;
+        return FTAR_SUCCESS;
+    }
+    memset(job, 0, sizeof(*job));
+    snprintf(job->name, sizeof(job->name), "%s", name);
+    double t0 = now_s();
+    for (;;) {
+        int fd = shm_open(name, O_RDWR, 0600);
+        if (fd >= 0) {
+            struct stat st;
+            if (fstat(fd, &st) == 0 && (size_t)st.st_size >= sizeof(ftar_shm)) {
+                int rc = map_segment(job, fd);
+                close(fd);
+                if (rc) return rc;
+                while (!atomic_load_explicit(&job->shm->ready, memory_order_acquire)) {
+                    if (now_s() - t0 > 120.0) return FTAR_ERR_STATE;
+                    usleep(1000);
+                }
+                break;
+            }
+            close(fd);
+        }
+        if (now_s() - t0 > 120.0) {
+            fprintf(stderr, "ftar: rank %d: control block %s never appeared\n", rank, name);
+            return FTAR_ERR_STATE;
+        }
+        usleep(1000);
+    }
+    if (job->shm->magic != FTAR_SHM_MAGIC || job->shm->size != size) return FTAR_ERR_STATE;
+    job->rank = rank;
+    job->size = size;
+    return FTAR_SUCCESS;
+}
+
+int ftar_ctrl_join(ftar_job *job, int device)
+{
+    ftar_slot *s = &job->shm->slot[job->rank];
+    pthread_mutexattr_t a;
+    pthread_mutexattr_init(&a);
+    pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+    pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST);
+    if (pthread_mutex_init(&s->alive, &a) != 0) return FTAR_ERR_STATE;
+    pthread_mutexattr_destroy(&a);
+    if (pthread_mutex_lock(&s->alive) != 0) return FTAR_ERR_STATE;
+    s->device = device;
+    atomic_store(&s->pid, (int)getpid());
+    atomic_store(&s->arrive, 0);
+    atomic_store_explicit(&s->state, FTAR_SLOT_RUNNING, memory_order_release);
+    job->seq = 0;
+    return FTAR_SUCCESS;
+}
+
+void ftar_ctrl_leave(ftar_job *job)
+{
+    if (!job->shm || job->rank < 0) return;
+    ftar_slot *s = &job->shm->slot[job->rank];
+    atomic_store_explicit(&s->state, FTAR_SLOT_FINALIZED, memory_order_release);
+    pthread_mutex_unlock(&s->alive);
+    atomic_fetch_add(&job->shm->nfinalized, 1);
+}
+
+void ftar_ctrl_detach(ftar_job *job)
+{
+    if (job->shm) munmap(job->shm, sizeof(ftar_shm));
+    job->shm = NULL;
+}
+
+uint64_t ftar_ctrl_failed(ftar_job *job)
+{
+    return atomic_load_explicit(&job->shm->failed, memory_order_acquire);
+}
+
+static void mark_failed(ftar_job *job, int m)
+{
+    atomic_fetch_or_explicit(&job->shm->failed, 1ull << m, memory_order_acq_rel);
+}
+
+int ftar_ctrl_is_dead(ftar_job *job, int m)
+{
+    if (ftar_ctrl_failed(job) & (1ull << m)) return 1;
+    ftar_slot *s = &job->shm->slot[m];
+    if (atomic_load_explicit(&s->state, memory_order_acquire) != FTAR_SLOT_RUNNING) return 0;
+    int r = pthread_mutex_trylock(&s->alive);
+    if (r == EBUSY) return 0;
+    if (r == EOWNERDEAD || r == ENOTRECOVERABLE) {
+        mark_failed(job, m);
+        if (r == EOWNERDEAD) pthread_mutex_unlock(&s->alive); /* leaves it not recoverable */
+        return 1;
+    }
+    if (r == 0) {
+        /* the owner released it: it finalized cleanly between our two reads */
+        pthread_mutex_unlock(&s->alive);
+        return 0;
+    }
+    int pid = atomic_load(&s->pid);
+    if (pid > 0 && kill(pid, 0) != 0 && errno == ESRCH) {
+        mark_failed(job, m);
+        return 1;
+    }
+    return 0;
+}
+
+static void exit_aborted(ftar_job *job)
+{
+    int code = atomic_load(&job->shm->abort_code);
+    fflush(stdout);
+    _exit(code ? code : 1);
+}
+
+int ftar_ctrl_poll(void *arg)
+{
+    ftar_job *job = (ftar_job *)arg;
+    if (atomic_load_explicit(&job->shm->abort_flag, memory_order_acquire)) exit_aborted(job);
+    return 0;
+}
+
+/* Every member other than self has arrived at `seq` or is dead? */
+static int round_complete(ftar_job *job, uint64_t members, uint64_t seq, double t0)
+{
+    for (int m = 0; m < job->size; m++) {
+        if (!(members & (1ull << m)) || m == job->rank) continue;
+        ftar_slot *s = &job->shm->slot[m];
+        if (atomic_load_explicit(&s->arrive, memory_order_acquire) >= seq) continue;
+        if (ftar_ctrl_is_dead(job, m)) continue;
+        if (atomic_load_explicit(&s->state, memory_order_acquire) == FTAR_SLOT_EMPTY && now_s() - t0 > 120.0) {
+            fprintf(stderr, "ftar: rank %d never joined the job\n", m);
+            ftar_ctrl_abort(job, FTAR_ERR_STATE);
+        }
+        return 0;
+    }
+    return 1;
+}
+
+uint64_t ftar_ctrl_agree(ftar_job *job, uint64_t members)
+{
+    ftar_shm *S = job->shm;
+    uint64_t seq = ++job->seq;
+    atomic_store_explicit(&S->slot[job->rank].arrive, seq, memory_order_release);
+    unsigned idx = (unsigned)(seq % FTAR_DECISIONS);
+    double t0 = now_s();
+    for (unsigned long it = 0;; it++) {
+        if (atomic_load_explicit(&S->abort_flag, memory_order_acquire)) exit_aborted(job);
+        uint64_t w = atomic_load_explicit(&S->decision[idx], memory_order_acquire);
+        if (w & FTAR_DECIDED) return w & ~FTAR_DECIDED;
+        if (round_complete(job, members, seq, t0)) {
+            uint64_t snap = ftar_ctrl_failed(job) & members & ~FTAR_DECIDED;
+            uint64_t expect = 0;
+            if (atomic_compare_exchange_strong_explicit(&S->decision[idx], &expect, snap | FTAR_DECIDED,
+                                                        memory_order_acq_rel, memory_order_acquire)) {
+                /* every live member has read round seq-1 before arriving here: recycle it */
+                atomic_store_explicit(&S->decision[(seq - 1) % FTAR_DECISIONS], 0, memory_order_release);
+            }
+            continue;
+        }
+        cpu_relax();
+    }
+}
+
+void ftar_ctrl_wait_peers_arrived(ftar_job *job, uint64_t members, uint64_t seq)
+{
+    double t0 = now_s();
+    while (!round_complete(job, members, seq, t0)) {
+        if (atomic_load_explicit(&job->shm->abort_flag, memory_order_acquire)) exit_aborted(job);
+        cpu_relax();
+    }
+}
+
+void ftar_ctrl_abort(ftar_job *job, int code)
+{
+    ftar_shm *S = job->shm;
+    int expect = 0;
+    fflush(stdout);
+    if (atomic_compare_exchange_strong(&S->abort_flag, &expect, 1)) {
+        atomic_store(&S->abort_code, code);
+        atomic_store(&S->abort_rank, job->rank);
+        fprintf(stderr,
+                "--------------------------------------------------------------------------\n"
+                "MPI_ABORT was invoked on rank %d in communicator MPI_COMM_WORLD\n"
+                "with errorcode %d.\n"
+                "--------------------------------------------------------------------------\n",
+                job->rank, code);
+        fflush(stderr);
+        /* like Open MPI's MPI_Abort: take every process of the job down */
+        for (int m = 0; m < job->size; m++) {
+            if (m == job->rank) continue;
+            ftar_slot *s = &S->slot[m];
+            int pid = atomic_load(&s->pid);
+            if (pid > 0 && atomic_load(&s->state) == FTAR_SLOT_RUNNING) kill(pid, SIGKILL);
+        }
+    }
+    _exit(code ? code : 1);
+}

@@ -1,0 +1,100 @@
+/*
+ * ftar_ctrl.h -- per-job shared-memory control plane (host C, no MPI, no HIP).
+ *
+ * Replaces the ULFM runtime services the reference relies on:
+ *   failure detection   -> one process-shared robust mutex per rank, held for the
+ *                          rank's lifetime; the kernel releases it with OWNER_DIED the
+ *                          instant the process dies (kill -9 included), so a probe
+ *                          (trylock) is an authoritative, immediate death test;
+ *   MPIX_Comm_agree     -> ftar_ctrl_agree(): a round completes when every member has
+ *   + MPI_Barrier          arrived or is dead; the first rank that sees completion seals
+ *                          the round's failure snapshot with one CAS, so every survivor
+ *                          returns the same set (uniform, unlike a bare ULFM barrier);
+ *   MPI_Abort           -> abort flag + SIGKILL of every rank (and the launcher's reaper);
+ *   exchange of IPC memory handles and per-step publications (RD's accumulator id).
+ */
+#ifndef FTAR_CTRL_H
+#define FTAR_CTRL_H
+
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <sys/types.h>
+
+#include "../../include/ftar.h"
+#include "ftar_dev.h"
+
+#define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
+#define FTAR_SHM_VERSION 1
+#define FTAR_NBUF 3       /* exported workspace buffers per rank */
+#define FTAR_DECISIONS 64 /* ring of agree decisions */
+
+#define FTAR_SLOT_EMPTY 0
+#define FTAR_SLOT_RUNNING 2
+#define FTAR_SLOT_FINALIZED 3
+
+#define FTAR_DECIDED (1ull << 63)
+
+typedef struct {
+    pthread_mutex_t alive;          /* robust + pshared, locked by the owner while alive */
+    _Atomic int state;              /* FTAR_SLOT_* */
+    _Atomic int pid;
+    int device;
+    _Atomic uint64_t arrive;        /* last agree sequence number this rank arrived at */
+    _Atomic uint64_t ws_gen;        /* generation of the exported workspace */
+    uint64_t ws_bytes;
+    unsigned char handle[FTAR_NBUF][FDEV_HANDLE_BYTES];
+    /* per-round publication (RD: which buffer holds the accumulator), double-buffered by
+     * round parity: written before arriving at round s into pubv[s % 2] tagged s */
+    _Atomic uint64_t pubv[2];
+    char pad[64];
+} ftar_slot;
+
+typedef struct {
+    uint32_t magic;
+    uint32_t version;
+    int size;
+    _Atomic int ready;
+    _Atomic uint64_t failed;        /* one bit per original rank, monotone */
+    _Atomic int abort_flag;
+    _Atomic int abort_code;
+    _Atomic int abort_rank;
+    _Atomic int nfinalized;
+    _Atomic int launcher_pid;       /* ftrun pid when launched by it, else 0 */
+    _Atomic uint64_t decision[FTAR_DECISIONS];
+    ftar_slot slot[FTAR_MAX_RANKS];
+} ftar_shm;
+
+typedef struct {
+    ftar_shm *shm;
+    char name[128];
+    int rank;     /* original rank = slot index */
+    int size;
+    uint64_t seq; /* agree sequence number */
+    int owner;    /* created the segment */
+} ftar_job;
+
+/* Create (launcher / rank 0) or attach (others) the segment named `name`. */
+int ftar_ctrl_create(ftar_job *job, const char *name, int size);
+int ftar_ctrl_attach(ftar_job *job, const char *name, int rank, int size, int create_if_rank0);
+/* Claim this rank's slot: robust mutex locked, pid, state RUNNING. */
+int ftar_ctrl_join(ftar_job *job, int device);
+void ftar_ctrl_leave(ftar_job *job);
+void ftar_ctrl_detach(ftar_job *job);
+
+/* Is original rank m dead?  (failed bit, else robust-mutex probe; marks the bit) */
+int ftar_ctrl_is_dead(ftar_job *job, int m);
+uint64_t ftar_ctrl_failed(ftar_job *job);
+
+/* Agree round over `members` (bit mask of original ranks, must contain self).
+ * Returns the sealed failure snapshot (subset of members).  Never returns on abort. */
+uint64_t ftar_ctrl_agree(ftar_job *job, uint64_t members);
+/* Block until every member other than self arrived at round `seq` or is dead. */
+void ftar_ctrl_wait_peers_arrived(ftar_job *job, uint64_t members, uint64_t seq);
+
+/* MPI_Abort: flag the job, print the OpenMPI-style line on stderr, kill all ranks. */
+void ftar_ctrl_abort(ftar_job *job, int code) __attribute__((noreturn));
+/* Nonzero if the job is aborting (the caller then exits). */
+int ftar_ctrl_poll(void *job);
+
+#endif

@@ -1,0 +1,95 @@
+/*
+ * ftar_dev.h -- the device layer the host C schedules call (internal to libftar).
+ *
+ * One ftar_dev per rank process: the HIP device it drives, one non-blocking stream
+ * the schedules enqueue on, exportable (IPC) allocations, and the segment kernel.
+ * Implemented in ftar_dev_hip.cpp + ftar_kernels.hip.  The schedules never see a HIP
+ * type: everything crosses this header as plain pointers and sizes.
+ */
+#ifndef FTAR_DEV_H
+#define FTAR_DEV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FDEV_HANDLE_BYTES 64
+
+/* One piece of work of a segment kernel.
+ *   FDEV_COPY:   out[i] = x[i]
+ *   FDEV_REDUCE: out[i] = x[i] <op> y[i]; x has the MPI "inout" role and y the "in"
+ *                role of MPI_Reduce_local(in=y, inout=x) (matters only for MAX/MIN
+ *                with NaN or signed zeros; SUM/PROD are commutative bit for bit).
+ * `out` may alias `x` (in-place reduce).  Pointers may be peer (xGMI) mappings. */
+#define FDEV_COPY 0
+#define FDEV_REDUCE 1
+
+#define FDEV_REMOTE_X 1
+#define FDEV_REMOTE_Y 2
+
+typedef struct {
+    int kind;
+    int remote;       /* FDEV_REMOTE_* bits, for the byte accounting only */
+    void *out;
+    const void *x;
+    const void *y;
+    size_t n;         /* elements */
+} fdev_seg;
+
+#define FDEV_MAX_SEGS 4
+
+/* kernel tags (profiling buckets) */
+#define FDEV_TAG_LOCAL 0   /* local copies */
+#define FDEV_TAG_STEP0 1   /* dominant exchange kernel: Raben RS step 0 / RD step */
+#define FDEV_TAG_STEP 2    /* other exchange kernels */
+#define FDEV_TAG_RECOV 3   /* recovery transfers */
+#define FDEV_NTAGS 4
+
+typedef struct ftar_dev ftar_dev;
+
+typedef struct {
+    double ms[FDEV_NTAGS];      /* device time per tag (profiling on) */
+    int launches[FDEV_NTAGS];
+    double link_bytes;          /* bytes read through peer mappings */
+    double hbm_bytes;           /* algorithmic local HBM bytes */
+} fdev_counters;
+
+int fdev_device_count(int *n);
+int fdev_open(int device, ftar_dev **out);
+void fdev_close(ftar_dev *d);
+int fdev_device(const ftar_dev *d);
+
+int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle /* FDEV_HANDLE_BYTES */);
+int fdev_free(ftar_dev *d, void *ptr);
+int fdev_import(ftar_dev *d, const void *handle, void **ptr);
+int fdev_unimport(ftar_dev *d, void *ptr);
+
+/* Enqueue one segment kernel on the rank's stream. */
+int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+/* Make the rank's stream wait for everything queued on `user_stream` (hipStream_t). */
+int fdev_order_after(ftar_dev *d, void *user_stream);
+/* Spin (busy, the process stays in R state) until the stream drained.  `poll` is
+ * called between queries; a nonzero return aborts the wait with that value. */
+int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg);
+
+int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t bytes);
+int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t bytes);
+int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr);
+
+void fdev_profiling(ftar_dev *d, int on);
+void fdev_counters_reset(ftar_dev *d);
+void fdev_counters_get(ftar_dev *d, fdev_counters *out);
+
+/* Standalone local reduce on a caller stream (MPI_Reduce_local). */
+int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream);
+int fdev_set_reduce_variant(int v);
+
+const char *fdev_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

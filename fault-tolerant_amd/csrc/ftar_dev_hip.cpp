@@ -1,0 +1,319 @@
+// ftar_dev_hip.cpp -- HIP runtime glue of libftar: device/stream setup, IPC (xGMI peer)
+// mappings, segment-kernel launches with optional hipEvent timing, busy-wait sync.
+//
+// One process per rank.  Peer buffers are exported with hipIpcGetMemHandle and mapped
+// with hipIpcOpenMemHandle(hipIpcMemLazyEnablePeerAccess); a kernel then reads a peer's
+// HBM directly over xGMI ("pull"), so a dead sender can never wedge a receiver's queue.
+
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "ftar_dev.h"
+#include "ftar_kernels.h"
+
+namespace {
+
+char g_err[512];
+int g_reduce_variant = 0;
+
+int set_err(hipError_t e, const char *what)
+{
+    snprintf(g_err, sizeof(g_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    return 101; // FTAR_ERR_DEVICE
+}
+
+#define HIPCHK(call)                                                                                        \
+    do {                                                                                                    \
+        hipError_t _e = (call);                                                                             \
+        if (_e != hipSuccess) return set_err(_e, #call);                                                    \
+    } while (0)
+
+size_t esize_of(int dtype)
+{
+    switch (dtype) {
+    case ftar::kInt32:
+    case ftar::kFloat32: return 4;
+    case ftar::kInt64:
+    case ftar::kFloat64: return 8;
+    default: return 0;
+    }
+}
+
+struct Pending {
+    hipEvent_t start, stop;
+    int tag;
+};
+
+} // namespace
+
+struct ftar_dev {
+    int device;
+    hipStream_t stream;
+    int profiling;
+    unsigned max_blocks;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+    fdev_counters ctr;
+};
+
+extern "C" {
+
+const char *fdev_last_error(void) { return g_err; }
+
+int fdev_device_count(int *n)
+{
+    HIPCHK(hipGetDeviceCount(n));
+    return 0;
+}
+
+int fdev_open(int device, ftar_dev **out)
+{
+    *out = nullptr;
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) {
+        snprintf(g_err, sizeof(g_err), "device %d out of range (%d visible)", device, ndev);
+        return 101;
+    }
+    HIPCHK(hipSetDevice(device));
+    ftar_dev *d = new ftar_dev();
+    d->device = device;
+    d->profiling = 0;
+    memset(&d->ctr, 0, sizeof(d->ctr));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    // 8 resident 256-thread workgroups per CU (32 waves/CU) for the streaming kernels
+    d->max_blocks = (unsigned)prop.multiProcessorCount * 8u;
+    if (d->max_blocks == 0) d->max_blocks = 2048;
+    HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    // Peer access to every other GPU of the node: the exchanges read peers' HBM.
+    for (int p = 0; p < ndev; p++) {
+        if (p == device) continue;
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, device, p) == hipSuccess && can) {
+            hipError_t e = hipDeviceEnablePeerAccess(p, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+        }
+    }
+    *out = d;
+    return 0;
+}
+
+void fdev_close(ftar_dev *d)
+{
+    if (!d) return;
+    (void)hipSetDevice(d->device);
+    (void)hipStreamSynchronize(d->stream);
+    for (auto &p : d->pending) {
+        (void)hipEventDestroy(p.start);
+        (void)hipEventDestroy(p.stop);
+    }
+    for (auto e : d->event_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+int fdev_device(const ftar_dev *d) { return d->device; }
+
+int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
+{
+    HIPCHK(hipSetDevice(d->device));
+    void *p = nullptr;
+    HIPCHK(hipMalloc(&p, bytes));
+    hipIpcMemHandle_t h;
+    hipError_t e = hipIpcGetMemHandle(&h, p);
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        return set_err(e, "hipIpcGetMemHandle");
+    }
+    memcpy(handle, &h, FDEV_HANDLE_BYTES);
+    *ptr = p;
+    return 0;
+}
+
+int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr)
+{
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipMalloc(ptr, bytes));
+    return 0;
+}
+
+int fdev_free(ftar_dev *d, void *ptr)
+{
+    if (!ptr) return 0;
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipFree(ptr));
+    return 0;
+}
+
+int fdev_import(ftar_dev *d, const void *handle, void **ptr)
+{
+    HIPCHK(hipSetDevice(d->device));
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, FDEV_HANDLE_BYTES);
+    HIPCHK(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return 0;
+}
+
+int fdev_unimport(ftar_dev *d, void *ptr)
+{
+    if (!ptr) return 0;
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipIpcCloseMemHandle(ptr));
+    return 0;
+}
+
+static hipEvent_t get_event(ftar_dev *d)
+{
+    if (!d->event_pool.empty()) {
+        hipEvent_t e = d->event_pool.back();
+        d->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    size_t es = esize_of(dtype);
+    if (es == 0 || op < 0 || op > 3 || nseg < 0 || nseg > FDEV_MAX_SEGS || tag < 0 || tag >= FDEV_NTAGS) {
+        snprintf(g_err, sizeof(g_err), "fdev_run: bad arguments");
+        return 13;
+    }
+    ftar::SegIn in[FDEV_MAX_SEGS];
+    for (int i = 0; i < nseg; i++) {
+        in[i].kind = segs[i].kind == FDEV_COPY ? ftar::kCopy : ftar::kReduce;
+        in[i].out = segs[i].out;
+        in[i].x = segs[i].x;
+        in[i].y = segs[i].y;
+        in[i].n = segs[i].n;
+        double b = (double)segs[i].n * (double)es;
+        int nread = segs[i].kind == FDEV_COPY ? 1 : 2;
+        int nremote = ((segs[i].remote & FDEV_REMOTE_X) ? 1 : 0) +
+                      ((segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) ? 1 : 0);
+        d->ctr.link_bytes += b * nremote;
+        d->ctr.hbm_bytes += b * (1 + nread - nremote);
+    }
+    ftar::KSegList L;
+    unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
+    if (grid == 0) return 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (d->profiling) {
+        e0 = get_event(d);
+        e1 = get_event(d);
+        if (e0) (void)hipEventRecord(e0, d->stream);
+    }
+    hipError_t e = ftar::launch_segments(dtype, op, L, grid, d->stream);
+    if (e != hipSuccess) return set_err(e, "segment_kernel launch");
+    if (d->profiling && e0 && e1) {
+        (void)hipEventRecord(e1, d->stream);
+        d->pending.push_back(Pending{e0, e1, tag});
+    }
+    return 0;
+}
+
+int fdev_order_after(ftar_dev *d, void *user_stream)
+{
+    hipEvent_t e = get_event(d);
+    if (!e) return set_err(hipErrorOutOfMemory, "hipEventCreate");
+    HIPCHK(hipEventRecord(e, (hipStream_t)user_stream));
+    HIPCHK(hipStreamWaitEvent(d->stream, e, 0));
+    d->event_pool.push_back(e); // safe: the wait was captured at enqueue time
+    return 0;
+}
+
+int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
+{
+    for (;;) {
+        hipError_t e = hipStreamQuery(d->stream);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return set_err(e, "hipStreamQuery");
+        if (poll) {
+            int r = poll(arg);
+            if (r) return r;
+        }
+    }
+    for (auto &p : d->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess) {
+            d->ctr.ms[p.tag] += ms;
+            d->ctr.launches[p.tag]++;
+        }
+        d->event_pool.push_back(p.start);
+        d->event_pool.push_back(p.stop);
+    }
+    d->pending.clear();
+    return 0;
+}
+
+int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t bytes)
+{
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d->stream));
+    return fdev_sync(d, nullptr, nullptr);
+}
+
+int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t bytes)
+{
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, d->stream));
+    return fdev_sync(d, nullptr, nullptr);
+}
+
+void fdev_profiling(ftar_dev *d, int on) { d->profiling = on; }
+
+void fdev_counters_reset(ftar_dev *d) { memset(&d->ctr, 0, sizeof(d->ctr)); }
+
+void fdev_counters_get(ftar_dev *d, fdev_counters *out) { *out = d->ctr; }
+
+int fdev_set_reduce_variant(int v)
+{
+    if (v < 0 || v > 1) return 13;
+    g_reduce_variant = v;
+    return 0;
+}
+
+int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream)
+{
+    size_t es = esize_of(dtype);
+    if (es == 0 || op < 0 || op > 3) {
+        snprintf(g_err, sizeof(g_err), "reduce_local: bad dtype/op");
+        return 13;
+    }
+    if (n == 0) return 0;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    static int cached_dev = -1;
+    static unsigned cached_blocks = 2048;
+    if (cached_dev != dev) {
+        HIPCHK(hipGetDeviceProperties(&prop, dev));
+        cached_blocks = (unsigned)prop.multiProcessorCount * 8u;
+        cached_dev = dev;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    bool aligned = (((uintptr_t)in | (uintptr_t)inout) & 15) == 0 && (n * es) % 16 == 0;
+    if (g_reduce_variant == 1 && aligned) {
+        size_t nv = n * es / 16;
+        size_t tiles = (nv + 1023) / 1024;
+        unsigned grid = tiles < cached_blocks ? (unsigned)tiles : cached_blocks;
+        hipError_t e = ftar::launch_reduce_lds(dtype, op, inout, in, nv, grid, s);
+        if (e != hipSuccess) return set_err(e, "reduce_lds_kernel launch");
+        return 0;
+    }
+    // MPI_Reduce_local(in, inout): inout = inout <op> in  -> x = inout, y = in
+    ftar::SegIn seg{ftar::kReduce, inout, inout, in, n};
+    ftar::KSegList L;
+    unsigned grid = ftar::plan_segments(&seg, 1, es, cached_blocks, &L);
+    if (grid == 0) return 0;
+    hipError_t e = ftar::launch_segments(dtype, op, L, grid, s);
+    if (e != hipSuccess) return set_err(e, "segment_kernel launch");
+    return 0;
+}
+
+} // extern "C"

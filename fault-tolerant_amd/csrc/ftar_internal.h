@@ -1,0 +1,94 @@
+/*
+ * ftar_internal.h -- the communicator and helpers shared by the two schedules.
+ */
+#ifndef FTAR_INTERNAL_H
+#define FTAR_INTERNAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/ftar.h"
+#include "ftar_ctrl.h"
+#include "ftar_dev.h"
+
+/* workspace buffers (exported to every peer) */
+#define WS_IN 0  /* this rank's input vector (Raben: after the pre-step) */
+#define WS_W 1   /* accumulator: Raben rbuf, RD ping-pong A */
+#define WS_T 2   /* Raben tmp (step-0 redundancy copy), RD ping-pong B */
+
+
+struct ftar_comm {
+    ftar_job job;
+    int wrank, wsize; /* original rank / size (Data.original_rank/_size) */
+    int device;
+    ftar_dev *dev;
+    void *user_stream;
+
+    /* current communicator: comm rank -> original rank */
+    int order[FTAR_MAX_RANKS];
+    int size;
+    uint64_t members; /* survivors (bit per original rank) */
+    uint64_t acked;   /* failures already acknowledged (MPIX_Comm_failure_ack) */
+
+    ftar_kill kills[FTAR_MAX_KILLS];
+    int nkills;
+
+    /* exported workspace and the peers' mappings of theirs */
+    void *ws[FTAR_NBUF];
+    size_t ws_bytes;
+    void *peer[FTAR_MAX_RANKS][FTAR_NBUF];
+    size_t peer_bytes[FTAR_MAX_RANKS];
+
+    /* host staging for the _host entry points */
+    void *hsend, *hrecv;
+    size_t hbytes;
+
+    int64_t pubval; /* value published at every sync (RD: accumulator buffer id) */
+
+    int profiling;
+    ftar_stats stats;
+    int verbose;
+};
+
+size_t ftar_esize(int dtype);
+int ftar_my_comm_rank(const ftar_comm *c);
+int ftar_comm_rank_of(const ftar_comm *c, int w);
+
+/* collective: grow the exported workspace to hold `bytes` per buffer */
+int ftar_ensure_workspace(ftar_comm *c, size_t bytes);
+/* pointer to buffer b of original rank w (own or peer mapping) */
+void *ftar_buf(ftar_comm *c, int w, int b);
+
+/* agree over the survivors; returns newly failed original ranks (not yet acked) */
+uint64_t ftar_sync(ftar_comm *c);
+/* value original rank w published before the last completed sync */
+int64_t ftar_peer_pub(ftar_comm *c, int w);
+/* agree outside the tolerant region: any new failure aborts the job */
+void ftar_sync_fatal(ftar_comm *c);
+/* drain the device stream (busy wait, abort-aware) */
+int ftar_drain(ftar_comm *c);
+/* enqueue one segment kernel */
+int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+int ftar_is_dead(ftar_comm *c, int w);
+
+/* deterministic fault injection at (phase, step, point) */
+void ftar_maybe_die(ftar_comm *c, int phase, int step, int point);
+
+/* remove `dead` (comm rank), moving the entry at comm rank `repl` into its place */
+void ftar_regroup(ftar_comm *c, int dead, int repl);
+/* drop failed ranks from the survivor world keeping the order */
+void ftar_shrink(ftar_comm *c, uint64_t failed);
+
+void ftar_stats_begin(ftar_comm *c);
+void ftar_stats_end(ftar_comm *c);
+
+int ftar_hibit(int value, int start);
+int ftar_floor_pow2(int n);
+
+#define FTAR_CHECK(x)                                                                                       \
+    do {                                                                                                    \
+        int _rc = (x);                                                                                      \
+        if (_rc) return _rc;                                                                                \
+    } while (0)
+
+#endif

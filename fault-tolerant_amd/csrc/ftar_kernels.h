@@ -1,0 +1,44 @@
+// ftar_kernels.h -- internal interface between the HIP runtime glue and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace ftar {
+
+enum { kInt32 = 0, kFloat32 = 1, kInt64 = 2, kFloat64 = 3 };
+enum { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
+enum { kCopy = 0, kReduce = 1 };
+
+constexpr int kMaxKSegs = 12; // 4 user segments x (head, body, tail)
+
+struct KSeg {
+    void *out;
+    const void *x;
+    const void *y;
+    size_t n;
+    unsigned kind;
+    unsigned vec;
+    unsigned blk_begin;
+    unsigned blk_end;
+};
+
+struct KSegList {
+    KSeg s[kMaxKSegs];
+    int nseg;
+};
+
+struct SegIn {
+    int kind;
+    void *out;
+    const void *x;
+    const void *y;
+    size_t n;
+};
+
+unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_blocks, KSegList *L);
+hipError_t launch_segments(int dtype, int op, const KSegList &L, unsigned grid, hipStream_t s);
+hipError_t launch_reduce_lds(int dtype, int op, void *inout, const void *in, size_t nvec, unsigned grid,
+                             hipStream_t s);
+
+} // namespace ftar

@@ -1,0 +1,292 @@
+// ftar_kernels.hip -- CDNA4 (gfx950) kernels of the fault-tolerant Allreduce.
+//
+// Every kernel here is HBM- or xGMI-bound integer/float streaming work: one pass over
+// the operands, no reuse, no MFMA.  What matters on MI355X:
+//   * 16-byte lanes (global_load_dwordx4 / global_store_dwordx4): 1 KiB per wave
+//     instruction, the widest coalesced access;
+//   * enough bytes in flight: each lane issues UNROLL independent 16-byte loads per
+//     operand before it consumes any (128 B per lane for a reduce), and the grid holds
+//     up to 8 workgroups of 4 waves per CU (32 waves/CU);
+//   * one launch handles up to FDEV_MAX_KSEGS independent segments (e.g. Raben's
+//     step 0: reduce half the window + copy the other half of the partner's vector),
+//     blocks are split between segments in proportion to their bytes and each wave
+//     finds its segment with a wave-uniform (readfirstlane) search;
+//   * segments whose pointers are not co-aligned to 16 bytes are split by the host
+//     into a scalar head, a vector body and a scalar tail.
+// Peer (xGMI) pointers obtained through hipIpcOpenMemHandle are plain device pointers
+// here: the same kernel is the local reduce and the fused "pull + reduce" exchange.
+//
+// Reference semantics restated: MPI_Reduce_local(in, inout) = inout <op> in with
+// OpenMPI's operand roles (out = out + in; max: out = (out > in) ? out : in), see
+// include/ftar.h.  int32/int64 SUM/PROD wrap (two's complement), floats are one IEEE
+// op per element (-ffp-contract=off, no fast-math).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "ftar_kernels.h"
+
+namespace ftar {
+
+// ---------------------------------------------------------------------------------
+// element ops
+// ---------------------------------------------------------------------------------
+template <typename T> struct Arith { using U = T; };
+template <> struct Arith<int32_t> { using U = uint32_t; };
+template <> struct Arith<int64_t> { using U = uint64_t; };
+
+template <typename T, int OP>
+__device__ __forceinline__ T apply(T x, T y)
+{
+    using U = typename Arith<T>::U;
+    if constexpr (OP == kSum) return (T)((U)x + (U)y);
+    else if constexpr (OP == kProd) return (T)((U)x * (U)y);
+    else if constexpr (OP == kMax) return (x > y) ? x : y;
+    else return (x < y) ? x : y;
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ uint4 apply16(uint4 a, uint4 b)
+{
+    constexpr int E = 16 / sizeof(T);
+    T xa[E], xb[E];
+    __builtin_memcpy(xa, &a, 16);
+    __builtin_memcpy(xb, &b, 16);
+#pragma unroll
+    for (int e = 0; e < E; e++) xa[e] = apply<T, OP>(xa[e], xb[e]);
+    uint4 r;
+    __builtin_memcpy(&r, xa, 16);
+    return r;
+}
+
+// ---------------------------------------------------------------------------------
+// segment kernel
+// ---------------------------------------------------------------------------------
+constexpr int kBlock = 256;
+constexpr int kUnroll = 4;
+
+__device__ __forceinline__ int find_segment(const KSegList &L)
+{
+    // blockIdx is wave-uniform; readfirstlane keeps the search in SGPRs.
+    int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    int si = 0;
+    while (si + 1 < L.nseg && (unsigned)b >= L.s[si].blk_end) si++;
+    return __builtin_amdgcn_readfirstlane(si);
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk)
+{
+    constexpr size_t E = 16 / sizeof(T);
+    const uint4 *__restrict__ X = (const uint4 *)S.x;
+    const uint4 *__restrict__ Y = (const uint4 *)S.y;
+    uint4 *__restrict__ O = (uint4 *)S.out;
+    const size_t nv = S.n / E;
+    const size_t stride = nblk * kBlock;
+    size_t i = b * kBlock + threadIdx.x;
+    if (S.kind == kCopy) {
+        for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
+            uint4 a[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) a[u] = X[i + u * stride];
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) O[i + u * stride] = a[u];
+        }
+        for (; i < nv; i += stride) O[i] = X[i];
+    } else {
+        for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
+            uint4 a[kUnroll], c[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) a[u] = X[i + u * stride];
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) c[u] = Y[i + u * stride];
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) O[i + u * stride] = apply16<T, OP>(a[u], c[u]);
+        }
+        for (; i < nv; i += stride) O[i] = apply16<T, OP>(X[i], Y[i]);
+    }
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void scalar_body(const KSeg &S, size_t b, size_t nblk)
+{
+    const T *X = (const T *)S.x;
+    const T *Y = (const T *)S.y;
+    T *O = (T *)S.out;
+    const size_t stride = nblk * kBlock;
+    for (size_t i = b * kBlock + threadIdx.x; i < S.n; i += stride)
+        O[i] = (S.kind == kCopy) ? X[i] : apply<T, OP>(X[i], Y[i]);
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void segment_kernel(KSegList L)
+{
+    const int si = find_segment(L);
+    const KSeg &S = L.s[si];
+    const size_t nblk = S.blk_end - S.blk_begin;
+    const size_t b = blockIdx.x - S.blk_begin;
+    if (S.vec) vec_body<T, OP>(S, b, nblk);
+    else scalar_body<T, OP>(S, b, nblk);
+}
+
+// LDS-DMA staged local reduce (variant 1): the `in` operand is moved HBM -> LDS by
+// global_load_lds_dwordx4 (no VGPR destination; 1 KiB per wave instruction, landing at
+// the wave-uniform LDS base + 16 B x lane), the `inout` operand comes to VGPRs with
+// plain dwordx4 loads issued meanwhile.  Each wave reads back only what it staged, so
+// the only ordering needed is the wave's own vmcnt(0) -- no workgroup barrier.
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void reduce_lds_kernel(uint4 *__restrict__ inout,
+                                                            const uint4 *__restrict__ in, size_t nv)
+{
+    __shared__ uint4 stage[kUnroll * kBlock]; // 16 KiB per workgroup
+    const int wave = threadIdx.x >> 6;
+    const size_t tile = (size_t)kUnroll * kBlock;
+    for (size_t base = (size_t)blockIdx.x * tile; base < nv; base += (size_t)gridDim.x * tile) {
+        uint4 a[kUnroll];
+        if (base + tile <= nv) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) {
+                const uint4 *g = in + base + (size_t)u * kBlock + threadIdx.x;
+                uint4 *l = &stage[u * kBlock + wave * 64];
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                                 (__attribute__((address_space(3))) void *)l, 16, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) a[u] = inout[base + (size_t)u * kBlock + threadIdx.x];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++)
+                inout[base + (size_t)u * kBlock + threadIdx.x] =
+                    apply16<T, OP>(a[u], stage[u * kBlock + threadIdx.x]);
+        } else {
+            for (size_t i = base + threadIdx.x; i < nv; i += kBlock) inout[i] = apply16<T, OP>(inout[i], in[i]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------------
+template <typename T>
+static hipError_t launch_t(int op, const KSegList &L, unsigned grid, hipStream_t s)
+{
+    switch (op) {
+    case kSum: hipLaunchKernelGGL((segment_kernel<T, kSum>), dim3(grid), dim3(kBlock), 0, s, L); break;
+    case kProd: hipLaunchKernelGGL((segment_kernel<T, kProd>), dim3(grid), dim3(kBlock), 0, s, L); break;
+    case kMax: hipLaunchKernelGGL((segment_kernel<T, kMax>), dim3(grid), dim3(kBlock), 0, s, L); break;
+    case kMin: hipLaunchKernelGGL((segment_kernel<T, kMin>), dim3(grid), dim3(kBlock), 0, s, L); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_segments(int dtype, int op, const KSegList &L, unsigned grid, hipStream_t s)
+{
+    switch (dtype) {
+    case kInt32: return launch_t<int32_t>(op, L, grid, s);
+    case kFloat32: return launch_t<float>(op, L, grid, s);
+    case kInt64: return launch_t<int64_t>(op, L, grid, s);
+    case kFloat64: return launch_t<double>(op, L, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <typename T>
+static hipError_t launch_lds_t(int op, uint4 *inout, const uint4 *in, size_t nv, unsigned grid, hipStream_t s)
+{
+    switch (op) {
+    case kSum: hipLaunchKernelGGL((reduce_lds_kernel<T, kSum>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv); break;
+    case kProd: hipLaunchKernelGGL((reduce_lds_kernel<T, kProd>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv); break;
+    case kMax: hipLaunchKernelGGL((reduce_lds_kernel<T, kMax>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv); break;
+    case kMin: hipLaunchKernelGGL((reduce_lds_kernel<T, kMin>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_lds(int dtype, int op, void *inout, const void *in, size_t nvec, unsigned grid,
+                             hipStream_t s)
+{
+    uint4 *io = (uint4 *)inout;
+    const uint4 *i = (const uint4 *)in;
+    switch (dtype) {
+    case kInt32: return launch_lds_t<int32_t>(op, io, i, nvec, grid, s);
+    case kFloat32: return launch_lds_t<float>(op, io, i, nvec, grid, s);
+    case kInt64: return launch_lds_t<int64_t>(op, io, i, nvec, grid, s);
+    case kFloat64: return launch_lds_t<double>(op, io, i, nvec, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// Split user segments into co-aligned vector bodies + scalar heads/tails and assign
+// blocks.  Returns the grid size (0 if there is nothing to do).
+unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_blocks, KSegList *L)
+{
+    L->nseg = 0;
+    size_t vec_bytes_total = 0;
+    struct Piece { KSeg k; size_t bytes; } pieces[kMaxKSegs];
+    int np = 0;
+    for (int s = 0; s < nin; s++) {
+        const SegIn &g = in[s];
+        if (g.n == 0) continue;
+        uintptr_t ao = (uintptr_t)g.out, ax = (uintptr_t)g.x, ay = (uintptr_t)(g.kind == kCopy ? g.x : g.y);
+        bool co = ((ao & 15) == (ax & 15)) && ((ao & 15) == (ay & 15)) && (16 % esize == 0) &&
+                  ((ao & 15) % esize == 0);
+        size_t head = 0, body = 0;
+        if (co) {
+            size_t mis = ao & 15;
+            head = mis ? (16 - mis) / esize : 0;
+            if (head > g.n) head = g.n;
+            size_t rest = g.n - head;
+            size_t epv = 16 / esize;
+            body = (rest / epv) * epv;
+        }
+        size_t tail_off = head + body;
+        auto add = [&](size_t off, size_t n, unsigned vec) {
+            if (n == 0) return;
+            KSeg k;
+            k.out = (char *)g.out + off * esize;
+            k.x = (const char *)g.x + off * esize;
+            k.y = g.kind == kCopy ? k.x : (const void *)((const char *)g.y + off * esize);
+            k.n = n;
+            k.kind = (unsigned)g.kind;
+            k.vec = vec;
+            k.blk_begin = k.blk_end = 0;
+            pieces[np].k = k;
+            pieces[np].bytes = n * esize;
+            if (vec) vec_bytes_total += n * esize;
+            np++;
+        };
+        add(0, head, 0);
+        add(head, body, 1);
+        add(tail_off, g.n - tail_off, 0);
+    }
+    if (np == 0) return 0;
+    // blocks: scalar pieces get 1 block (they are < 16 bytes, or unaligned slow paths
+    // sized by their own length), vector pieces share the rest by bytes.
+    const size_t bytes_per_block_min = (size_t)kBlock * 16 * kUnroll; // one unrolled sweep
+    unsigned next = 0;
+    for (int i = 0; i < np; i++) {
+        KSeg &k = pieces[i].k;
+        size_t want;
+        if (k.vec) {
+            size_t share = vec_bytes_total ? (size_t)((double)max_blocks * (double)pieces[i].bytes /
+                                                     (double)vec_bytes_total)
+                                           : 1;
+            size_t need = (pieces[i].bytes + bytes_per_block_min - 1) / bytes_per_block_min;
+            want = need < share ? need : share;
+        } else {
+            size_t need = (k.n + kBlock - 1) / kBlock;
+            want = need < 64 ? need : 64;
+        }
+        if (want < 1) want = 1;
+        k.blk_begin = next;
+        k.blk_end = next + (unsigned)want;
+        next = k.blk_end;
+        L->s[L->nseg++] = k;
+    }
+    return next;
+}
+
+} // namespace ftar

@@ -1,0 +1,353 @@
+/*
+ * ftar_raben.c -- fault-tolerant Rabenseifner Allreduce on MI355X (per rank, host C).
+ *
+ * Restates src/raben/rabenseifner.c:3-395 and src/raben/errhandler.c:3-468 for ranks
+ * that own one GPU each.  Every MPI_Sendrecv + MPI_Reduce_local pair becomes ONE
+ * receiver-driven kernel that reads the partner's window straight out of its HBM
+ * over xGMI (IPC peer mapping) and reduces it into the local window:
+ *
+ *   RS step 0 (:206-211 full exchange + :231-237 reduce):
+ *       W[rw0] = IN[rw0] + peer.IN[rw0]        (reduce half)
+ *       T[sw0] = peer.IN[sw0]                  (redundancy copy for recovery)
+ *   RS step k>=1 (:219-237):  W[rwk] = W[rwk] + peer.W[rwk]
+ *   AG step k (:299-315):     W[swk] = peer.W[swk]
+ *
+ * Buffers (exported workspace, ftar_internal.h): IN = this rank's vector after the
+ * pre-step (the reference's sbuf after :128), W = rbuf, T = tmp_buf.  The reference's
+ * tmp also stages the step>=1 windows; here those are fused into the reduce, which
+ * leaves T holding the partner's vector where recovery reads it (:191-197).
+ * No rank ever writes a window a peer reads in the same step, and each step ends at
+ * the agree+barrier of the reference (:258-260, :330-332), so pulls need no locks.
+ *
+ * Deviations: sbuf is never written (IN is a private shadow); the
+ * impersonator accumulates the dead rank's replay in W's half it does not own yet,
+ * not in sbuf/tmp, so a second impersonation by the same rank stays correct; a
+ * recovery that needs redundancy a replacement rank never received aborts instead of
+ * replaying garbage; new_entry pulls only the dead rank's live window.
+ */
+#include "ftar_internal.h"
+
+#include <stdio.h>
+#include <string.h>
+
+#define MAXSTEPS 32
+
+typedef struct {
+    ftar_comm *c;
+    int dtype, op;
+    size_t es, count;
+    int steps, adjsize, rem;
+    int rank, vrank, corr, has_recov;
+    int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
+} rb_ctx;
+
+static int rb_real(const rb_ctx *x, int v) { return (v < x->rem) ? v * 2 : v + x->rem; }
+
+static void rb_vrank(rb_ctx *x)
+{
+    x->rank = ftar_my_comm_rank(x->c);
+    if (x->rank < 2 * x->rem) x->vrank = (x->rank % 2 == 0) ? x->rank / 2 : -1;
+    else x->vrank = x->rank - x->rem;
+}
+
+/* Windows of virtual rank v at every step (raben/rabenseifner.c:170-249).  The
+ * reference compares real ranks (rank < dest); the vrank->rank map is monotone, so
+ * that is bit s of v being 0. */
+static void rb_windows(int v, size_t count, int steps, int64_t *rindex, int64_t *sindex, int64_t *rcount,
+                       int64_t *scount)
+{
+    int64_t wsize = (int64_t)count;
+    rindex[0] = sindex[0] = 0;
+    for (int s = 0; s < steps; s++) {
+        int lower = !((v >> s) & 1);
+        if (lower) {
+            rcount[s] = wsize / 2;
+            scount[s] = wsize - rcount[s];
+            sindex[s] = rindex[s] + rcount[s];
+        } else {
+            scount[s] = wsize / 2;
+            rcount[s] = wsize - scount[s];
+            rindex[s] = sindex[s] + scount[s];
+        }
+        if (s + 1 < steps) {
+            rindex[s + 1] = rindex[s];
+            sindex[s + 1] = rindex[s];
+            wsize = rcount[s];
+        }
+    }
+}
+
+static void *at(const rb_ctx *x, void *base, int64_t idx) { return (char *)base + (size_t)idx * x->es; }
+
+static void run_reduce(rb_ctx *x, void *out, const void *xin, const void *yin, int64_t n, int remote, int tag)
+{
+    fdev_seg s = {FDEV_REDUCE, remote, out, xin, yin, (size_t)n};
+    ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
+}
+
+static void run_copy(rb_ctx *x, void *out, const void *src, int64_t n, int remote, int tag)
+{
+    fdev_seg s = {FDEV_COPY, remote, out, src, NULL, (size_t)n};
+    ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
+}
+
+/* errhandler_reduce_scatter (raben/errhandler.c:3-282) in pull form */
+static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
+{
+    ftar_comm *c = x->c;
+    int nf = __builtin_popcountll(newf);
+    c->acked |= newf; /* MPIX_Comm_failure_ack (:20-21) */
+    if (nf > 1 || fs == 0) ftar_abort(c, 1); /* :37-38 */
+    int dead_w = __builtin_ctzll(newf);
+    int dead = ftar_comm_rank_of(c, dead_w);
+    int idle_die = (dead < x->rem * 2 && dead % 2 == 1);
+    if (idle_die) { /* :50-76 */
+        ftar_regroup(c, dead, x->rem * 2 - 1);
+    } else {
+        int vdead = (dead < x->rem * 2) ? dead / 2 : dead - x->rem; /* :80-88 */
+        int org = rb_real(x, vdead ^ 1);                           /* :89-90 */
+        int new_entry = x->rem * 2 - 1;                            /* :207 */
+        if (new_entry == -1) ftar_abort(c, 1);                     /* :210-211 */
+        int org_w = c->order[org];
+        int64_t dri[MAXSTEPS], dsi[MAXSTEPS], drc[MAXSTEPS], dsc[MAXSTEPS];
+        rb_windows(vdead, x->count, x->steps, dri, dsi, drc, dsc);
+        if (x->rank == org) {
+            if (!x->has_recov) ftar_abort(c, 1); /* deviation: no step-0 copy to replay from */
+            /* replay the dead rank's steps 0..fs (:106-200) into W's half this rank sent at
+             * step 0 (= the dead rank's reduce window, unused here until the allgather) */
+            void *W = c->ws[WS_W], *IN = c->ws[WS_IN], *T = c->ws[WS_T];
+            run_reduce(x, at(x, W, dri[0]), at(x, IN, dri[0]), at(x, T, dri[0]), drc[0], 0, FDEV_TAG_RECOV);
+            for (int s = 1; s <= fs; s++) {
+                int pw = c->order[rb_real(x, vdead ^ (1 << s))];
+                void *PW = ftar_buf(c, pw, WS_W);
+                run_reduce(x, at(x, W, dri[s]), at(x, W, dri[s]), at(x, PW, dri[s]), drc[s], FDEV_REMOTE_Y,
+                           FDEV_TAG_RECOV);
+            }
+            ftar_drain(c);
+        }
+        ftar_sync_fatal(c); /* the dead rank's state is ready in org's W */
+        int cp = rb_real(x, vdead ^ (1 << fs));
+        void *OW = ftar_buf(c, org_w, WS_W);
+        if (x->rank == cp && x->corr) { /* :170-180: reduce the window the dead rank owed us */
+            void *W = c->ws[WS_W];
+            run_reduce(x, at(x, W, x->rindex[fs]), at(x, W, x->rindex[fs]), at(x, OW, x->rindex[fs]),
+                       x->rcount[fs], FDEV_REMOTE_Y, FDEV_TAG_RECOV);
+        }
+        if (x->rank == new_entry) { /* :213-241: take over the dead rank's role */
+            memcpy(x->rindex, dri, sizeof(dri));
+            memcpy(x->sindex, dsi, sizeof(dsi));
+            memcpy(x->rcount, drc, sizeof(drc));
+            memcpy(x->scount, dsc, sizeof(dsc));
+            void *W = c->ws[WS_W];
+            run_copy(x, at(x, W, dri[fs]), at(x, OW, dri[fs]), drc[fs], FDEV_REMOTE_X, FDEV_TAG_RECOV);
+            x->has_recov = 0;
+        }
+        ftar_drain(c);
+        ftar_sync_fatal(c);
+        ftar_regroup(c, dead, new_entry); /* :243-281 */
+    }
+    x->rem--; /* rabenseifner.c:268-283 */
+    rb_vrank(x);
+    x->corr = 0;
+    c->stats.recoveries++;
+}
+
+/* errhandler_allgather (raben/errhandler.c:284-468) in pull form */
+static void rb_handler_ag(rb_ctx *x, uint64_t newf, int fs)
+{
+    ftar_comm *c = x->c;
+    int nf = __builtin_popcountll(newf);
+    c->acked |= newf; /* MPIX_Comm_failure_ack (:300-301) */
+    if (nf > 1 || fs == x->steps - 1) ftar_abort(c, 1); /* :320-323 */
+    int dead_w = __builtin_ctzll(newf);
+    int dead = ftar_comm_rank_of(c, dead_w);
+    int idle_die = (dead < x->rem * 2 && dead % 2 == 1);
+    if (idle_die) {
+        ftar_regroup(c, dead, x->rem * 2 - 1);
+    } else {
+        int vdead = (dead < x->rem * 2) ? dead / 2 : dead - x->rem;
+        int org = rb_real(x, vdead ^ (x->adjsize >> 1)); /* :372-373 */
+        int new_entry = x->rem * 2 - 1;
+        if (new_entry == -1) ftar_abort(c, 1); /* :377-378 */
+        if (x->rank == new_entry) {
+            /* :381-398: the original partner's buffer and index arrays (equal to the dead
+             * rank's for every remaining step).  Only the part held after the allgather
+             * step fs is live: the reduce-scatter window of step fs-1, or all of it. */
+            rb_windows(vdead, x->count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+            int64_t off = 0, n = (int64_t)x->count;
+            if (fs >= 1) {
+                off = x->rindex[fs - 1];
+                n = x->rcount[fs - 1];
+            }
+            void *OW = ftar_buf(c, c->order[org], WS_W);
+            run_copy(x, at(x, c->ws[WS_W], off), at(x, OW, off), n, FDEV_REMOTE_X, FDEV_TAG_RECOV);
+            x->has_recov = 0;
+            ftar_drain(c);
+        }
+        ftar_sync_fatal(c);
+        int lp = rb_real(x, vdead ^ (1 << fs)); /* :400-414 */
+        if (x->rank == lp) {
+            void *NW = ftar_buf(c, c->order[new_entry], WS_W);
+            run_copy(x, at(x, c->ws[WS_W], x->sindex[fs]), at(x, NW, x->sindex[fs]), x->scount[fs], FDEV_REMOTE_X,
+                     FDEV_TAG_RECOV);
+            ftar_drain(c);
+        }
+        ftar_sync_fatal(c);
+        ftar_regroup(c, dead, new_entry);
+    }
+    x->rem--;
+    rb_vrank(x);
+    c->stats.recoveries++;
+}
+
+int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar_dtype dtype, ftar_op op,
+                                ftar_comm *c)
+{
+    if (!c) return FTAR_ERR_ARG;
+    rb_ctx X;
+    memset(&X, 0, sizeof(X));
+    rb_ctx *x = &X;
+    x->c = c;
+    x->dtype = (int)dtype;
+    x->op = (int)op;
+    x->es = ftar_esize(dtype);
+    x->count = count;
+    if (x->es == 0 || op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
+    x->steps = ftar_hibit(c->size, (int)(sizeof(int) * 8) - 1); /* :16-21 */
+    if (x->steps == -1) return FTAR_ERR_ARG;
+    if (count == 0) return FTAR_ERR_UNKNOWN; /* copy_buffer(count <= 0), util.c:40-43 */
+    if (count > (size_t)INT64_MAX / 16 || !sbuf || !rbuf) return FTAR_ERR_ARG;
+    x->adjsize = 1 << x->steps;
+    x->rem = c->size - x->adjsize;
+    x->has_recov = 1;
+    ftar_stats_begin(c);
+
+    size_t bytes = count * x->es;
+    ftar_ensure_workspace(c, bytes);
+    void *IN = c->ws[WS_IN], *W = c->ws[WS_W], *T = c->ws[WS_T];
+    fdev_order_after(c->dev, c->user_stream); /* sbuf may still be in flight on the caller's stream */
+    run_copy(x, IN, sbuf, (int64_t)count, 0, FDEV_TAG_LOCAL); /* rbuf = sbuf, :35-42 */
+    ftar_drain(c);
+    rb_vrank(x);
+
+    /* ---- pre-step (:61-139): failures are fatal here ---- */
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BEFORE);
+    ftar_sync_fatal(c); /* every IN is ready */
+    int64_t lh = (int64_t)count / 2, rh = (int64_t)count - lh;
+    if (x->rank < 2 * x->rem) {
+        if (x->rank % 2 != 0) { /* odd: reduce the right half with the even's right half */
+            void *P = ftar_buf(c, c->order[x->rank - 1], WS_IN);
+            run_reduce(x, at(x, IN, lh), at(x, IN, lh), at(x, P, lh), rh, FDEV_REMOTE_Y, FDEV_TAG_STEP);
+        } else { /* even: reduce the left half with the odd's left half */
+            void *P = ftar_buf(c, c->order[x->rank + 1], WS_IN);
+            run_reduce(x, IN, IN, P, lh, FDEV_REMOTE_Y, FDEV_TAG_STEP);
+        }
+        ftar_drain(c);
+        c->stats.steps++;
+    }
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
+    ftar_sync_fatal(c);
+    if (x->rank < 2 * x->rem && x->rank % 2 == 0) { /* even: receive the reduced right half (:120) */
+        void *P = ftar_buf(c, c->order[x->rank + 1], WS_IN);
+        run_copy(x, at(x, IN, lh), at(x, P, lh), rh, FDEV_REMOTE_X, FDEV_TAG_STEP);
+        ftar_drain(c);
+    }
+    if (x->vrank != -1)
+        rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+    ftar_sync_fatal(c); /* MPI_Barrier before the tolerant region (:166) */
+
+    /* ---- reduce-scatter (:170-284) ---- */
+    int step = 0;
+    for (int mask = 1; mask < x->adjsize; mask <<= 1, step++) {
+        if (x->vrank != -1) {
+            ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BEFORE);
+            int pw = c->order[rb_real(x, x->vrank ^ mask)];
+            if (ftar_is_dead(c, pw)) {
+                x->corr = 1; /* the exchange failed (:238-241) */
+            } else if (step == 0) {
+                void *PIN = ftar_buf(c, pw, WS_IN);
+                fdev_seg s[2] = {
+                    {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, x->rindex[0]), at(x, IN, x->rindex[0]),
+                     at(x, PIN, x->rindex[0]), (size_t)x->rcount[0]},
+                    {FDEV_COPY, FDEV_REMOTE_X, at(x, T, x->sindex[0]), at(x, PIN, x->sindex[0]), NULL,
+                     (size_t)x->scount[0]},
+                };
+                ftar_run(c, x->dtype, x->op, s, 2, FDEV_TAG_STEP0);
+                ftar_drain(c);
+            } else {
+                void *PW = ftar_buf(c, pw, WS_W);
+                run_reduce(x, at(x, W, x->rindex[step]), at(x, W, x->rindex[step]), at(x, PW, x->rindex[step]),
+                           x->rcount[step], FDEV_REMOTE_Y, FDEV_TAG_STEP);
+                ftar_drain(c);
+            }
+            c->stats.steps++;
+            ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_AFTER);
+        } else {
+            ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BEFORE);
+            ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_AFTER);
+        }
+        ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BARRIER);
+        uint64_t newf = ftar_sync(c); /* agree + barrier (:258-265) */
+        if (newf) rb_handler_rs(x, newf, step);
+    }
+
+    /* ---- allgather (:299-355) ---- */
+    step = x->steps - 1;
+    for (int mask = x->adjsize >> 1; mask > 0; mask >>= 1, step--) {
+        ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BEFORE);
+        if (x->vrank != -1) {
+            int pw = c->order[rb_real(x, x->vrank ^ mask)];
+            if (!ftar_is_dead(c, pw)) {
+                void *PW = ftar_buf(c, pw, WS_W);
+                run_copy(x, at(x, W, x->sindex[step]), at(x, PW, x->sindex[step]), x->scount[step], FDEV_REMOTE_X,
+                         FDEV_TAG_STEP);
+                ftar_drain(c);
+            }
+            c->stats.steps++;
+        }
+        ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_AFTER);
+        ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BARRIER);
+        uint64_t newf = ftar_sync(c);
+        if (newf) rb_handler_ag(x, newf, step);
+    }
+
+    /* ---- ERRORS_ARE_FATAL barrier + post-step (:357-381) ---- */
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
+    ftar_sync_fatal(c);
+    if (x->rank < 2 * x->rem && x->rank % 2 != 0) {
+        void *P = ftar_buf(c, c->order[x->rank - 1], WS_W); /* odd: result from rank-1 */
+        run_copy(x, rbuf, P, (int64_t)count, FDEV_REMOTE_X, FDEV_TAG_STEP);
+        c->stats.steps++;
+    } else { /* with one rank there is no exchange and rbuf = sbuf (:35-42) */
+        run_copy(x, rbuf, x->steps == 0 ? IN : W, (int64_t)count, 0, FDEV_TAG_LOCAL);
+    }
+    ftar_drain(c);
+    ftar_sync_fatal(c); /* peers are done reading our W before it is reused */
+    ftar_stats_end(c);
+    return FTAR_SUCCESS;
+}
+
+int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count, ftar_dtype dtype, ftar_op op,
+                                     ftar_comm *c)
+{
+    if (!c) return FTAR_ERR_ARG;
+    size_t es = ftar_esize(dtype);
+    if (es == 0) return FTAR_ERR_ARG;
+    size_t bytes = count * es;
+    if (bytes > c->hbytes) {
+        fdev_free(c->dev, c->hsend);
+        fdev_free(c->dev, c->hrecv);
+        c->hsend = c->hrecv = NULL;
+        if (fdev_alloc_plain(c->dev, bytes, &c->hsend) || fdev_alloc_plain(c->dev, bytes, &c->hrecv))
+            return FTAR_ERR_NOMEM;
+        c->hbytes = bytes;
+    }
+    if (bytes && fdev_h2d(c->dev, c->hsend, sbuf, bytes)) return FTAR_ERR_DEVICE;
+    int rc = ftar_allreduce_rabenseifner(c->hsend, c->hrecv, count, dtype, op, c);
+    if (rc) return rc;
+    if (bytes && fdev_d2h(c->dev, rbuf, c->hrecv, bytes)) return FTAR_ERR_DEVICE;
+    return FTAR_SUCCESS;
+}

@@ -1,0 +1,286 @@
+/*
+ * ftar_rd.c -- fault-tolerant recursive-doubling Allreduce on MI355X (per rank, host C).
+ *
+ * Restates src/rd/recursive_doubling.c:6-90, src/rd/util.c:3-95 and
+ * src/rd/errhandler.c:6-302.  Each MPI_Sendrecv + MPI_Reduce_local of a step becomes
+ * one kernel that reads the partner's accumulator over xGMI and writes the sum into
+ * this rank's other ping-pong buffer:
+ *
+ *   middle steps (:42-49, Reduce_local(dst, src)):  A' = A + peer.A
+ *   last step    (:42-44, Reduce_local(src, dst)):  A' = peer.A + A   (operand roles kept)
+ *
+ * The reference accumulates in src (clobbering it) and receives into dst; here src is
+ * never written: the accumulator ping-pongs between the exported buffers W and T and
+ * each rank publishes which one holds its value at every barrier, so a peer never
+ * reads a buffer that is being written.
+ *
+ * Data (rd/header.h:16-26) is call-local: active/inactive lists of original ranks,
+ * identical on every rank because every rank applies the same decisions to the same
+ * agreed failure set.
+ *
+ * Deviation: the master search of the spare branch (errhandler.c:96-111)
+ * never advances `j` and loops forever; the build implements its evident intent (the
+ * master of each block of distance/2 ranks is its first rank that is alive and whose
+ * partner of the failed step is alive).  Cases where the reference reads
+ * uninitialised ranks or waits forever in the fan-out abort instead.
+ */
+#include "ftar_internal.h"
+
+#include <stdio.h>
+#include <string.h>
+
+typedef struct {
+    ftar_comm *c;
+    int dtype, op;
+    size_t es, count;
+    int active[FTAR_MAX_RANKS], nactive;
+    int inactive[FTAR_MAX_RANKS], ninactive;
+    int cur; /* WS_* buffer holding this rank's accumulator */
+} rd_ctx;
+
+static int index_of(const int *a, int n, int w)
+{
+    for (int i = 0; i < n; i++)
+        if (a[i] == w) return i;
+    return -1;
+}
+
+static int in_set(uint64_t set, int w) { return (int)((set >> w) & 1u); }
+
+/* the accumulator's buffer id is published at every sync (ftar_sync) and read back
+ * for the round that just completed, so a fast rank's next value never races a slow
+ * reader */
+static void publish_cur(rd_ctx *x) { x->c->pubval = x->cur; }
+
+static int peer_cur(rd_ctx *x, int w) { return (int)ftar_peer_pub(x->c, w); }
+
+static void run1(rd_ctx *x, int kind, void *out, const void *a, const void *b, int remote, int tag)
+{
+    fdev_seg s = {kind, remote, out, a, b, x->count};
+    ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
+}
+
+/* pull the accumulator of original rank `from` into a free buffer of this rank */
+static void restore_from(rd_ctx *x, int from)
+{
+    ftar_comm *c = x->c;
+    int dst = (x->cur == WS_IN) ? WS_W : x->cur;
+    run1(x, FDEV_COPY, c->ws[dst], ftar_buf(c, from, peer_cur(x, from)), NULL, FDEV_REMOTE_X, FDEV_TAG_RECOV);
+    x->cur = dst;
+}
+
+/* errhandler (rd/errhandler.c:6-302); `distance` is the caller's doubled distance.
+ * Returns the possibly reduced distance. */
+static int rd_handler(rd_ctx *x, uint64_t F, int distance)
+{
+    ftar_comm *c = x->c;
+    int d = distance / 2;
+    int nf = __builtin_popcountll(F);
+    int me = c->wrank;
+
+    /* shift out failed inactive ranks (:47-65) */
+    int inactive_nf = 0, k = 0;
+    for (int i = 0; i < x->ninactive; i++) {
+        if (in_set(F, x->inactive[i])) inactive_nf++;
+        else x->inactive[k++] = x->inactive[i];
+    }
+    x->ninactive = k;
+
+    int active_failed = 0;
+    for (int i = 0; i < x->nactive; i++)
+        if (in_set(F, x->active[i])) active_failed = 1;
+
+    if (active_failed) {
+        int nfa = nf - inactive_nf;
+        if (nfa >= d) { /* check_abort (util.c:49-78) */
+            int cnt = 0;
+            for (int i = 0; i < x->nactive; i++) {
+                if (i % distance == 0) cnt = 0;
+                if (in_set(F, x->active[i]) || in_set(F, x->active[i ^ d])) cnt++;
+                if (cnt == distance) ftar_abort(c, FTAR_ERR_OTHER);
+            }
+        }
+        if (nfa <= x->ninactive) {
+            /* spare branch (:78-177): wake spares, restore corrupted partners */
+            int master[FTAR_MAX_RANKS];
+            for (int b = 0; b * d < x->nactive; b++) {
+                master[b] = -1;
+                for (int i = b * d; i < (b + 1) * d && i < x->nactive; i++)
+                    if (!in_set(F, x->active[i]) && !in_set(F, x->active[i ^ d])) {
+                        master[b] = i;
+                        break;
+                    }
+            }
+            int j = x->ninactive - 1;
+            for (int i = 0; i < x->nactive; i++) {
+                if (!in_set(F, x->active[i])) continue;
+                int m = master[i / d];
+                if (m < 0) ftar_abort(c, FTAR_ERR_OTHER); /* no healthy rank to restore from */
+                int spare = x->inactive[j];
+                if (me == spare) restore_from(x, x->active[m]); /* woken (:240-244) */
+                int corr = i ^ d;
+                if (!in_set(F, x->active[corr])) { /* corrupted partner (:147-162, :245-249) */
+                    int mc = master[corr / d];
+                    if (mc < 0) ftar_abort(c, FTAR_ERR_OTHER);
+                    if (me == x->active[corr]) restore_from(x, x->active[mc]);
+                }
+                x->active[i] = spare;
+                j--;
+            }
+            x->ninactive = j + 1;
+            ftar_drain(c);
+            publish_cur(x);
+        } else {
+            /* shrink to the next lower power of two (:178-217) */
+            int p = ftar_floor_pow2(x->nactive - nfa);
+            int kk = x->nactive / p;
+            int newdist = distance / kk;
+            int blk = newdist * kk;
+            int newarr[FTAR_MAX_RANKS], total = 0, bc = 0;
+            int extra[FTAR_MAX_RANKS], nextra = 0;
+            for (int i = 0; i < x->nactive; i++) {
+                if (i % blk == 0) bc = 0;
+                if (in_set(F, x->active[i])) continue;
+                if (bc < newdist && !in_set(F, x->active[i ^ (blk / 2)])) {
+                    newarr[total++] = x->active[i];
+                    bc++;
+                } else {
+                    extra[nextra++] = x->active[i];
+                }
+            }
+            if (total < p) ftar_abort(c, FTAR_ERR_OTHER); /* reference: uninitialised ranks */
+            for (int i = 0; i < nextra; i++) x->inactive[x->ninactive++] = extra[i];
+            memcpy(x->active, newarr, sizeof(int) * (size_t)p);
+            x->nactive = p;
+            distance = newdist;
+        }
+    }
+    c->acked |= F;
+    ftar_shrink(c, F); /* MPIX_Comm_shrink of the world (:43-45) */
+    ftar_sync_fatal(c); /* errhandler's closing barrier (:299) */
+    c->stats.recoveries++;
+    return distance;
+}
+
+int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype dtype, ftar_op op, ftar_comm *c)
+{
+    if (!c) return FTAR_ERR_ARG;
+    rd_ctx X;
+    memset(&X, 0, sizeof(X));
+    rd_ctx *x = &X;
+    x->c = c;
+    x->dtype = (int)dtype;
+    x->op = (int)op;
+    x->es = ftar_esize(dtype);
+    x->count = count;
+    if (x->es == 0 || op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
+    if (count && (!src || !dst)) return FTAR_ERR_ARG;
+    if (count == 0) return FTAR_SUCCESS;
+    ftar_stats_begin(c);
+    int me = c->wrank;
+
+    ftar_ensure_workspace(c, count * x->es);
+    fdev_order_after(c->dev, c->user_stream);
+    run1(x, FDEV_COPY, c->ws[WS_IN], src, NULL, 0, FDEV_TAG_LOCAL);
+    ftar_drain(c);
+    x->cur = WS_IN;
+    publish_cur(x);
+
+    /* Data + reduce_pow2 (recursive_doubling.c:118-130, util.c:3-34) */
+    int size = c->size;
+    int pp = ftar_floor_pow2(size);
+    x->nactive = pp;
+    for (int i = 0; i < pp; i++) x->active[i] = c->order[i];
+    x->ninactive = size - pp;
+    for (int i = pp; i < size; i++) x->inactive[i - pp] = c->order[i];
+    uint64_t involved = 0; /* ranks with a pre-step exchange (errors there are fatal) */
+    for (int r = 0; r < x->ninactive; r++) involved |= (1ull << x->active[r]) | (1ull << x->inactive[r]);
+
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BEFORE);
+    uint64_t newf = ftar_sync(c); /* every IN is ready */
+    if (newf & involved) ftar_abort(c, FTAR_ERR_PROC_FAILED);
+    int ia = index_of(x->active, x->nactive, me);
+    if (ia >= 0 && ia < x->ninactive) {
+        const void *P = ftar_buf(c, x->inactive[ia], WS_IN);
+        run1(x, FDEV_REDUCE, c->ws[WS_W], c->ws[WS_IN], P, FDEV_REMOTE_Y, FDEV_TAG_STEP); /* src = dst + src */
+        ftar_drain(c);
+        x->cur = WS_W;
+        publish_cur(x);
+        c->stats.steps++;
+    }
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
+    newf = ftar_sync(c); /* MPI_Barrier after switching to ERRORS_RETURN (:16-18) */
+    if (newf & involved) ftar_abort(c, FTAR_ERR_PROC_FAILED);
+
+    /* recursive doubling body (:21-71) */
+    int iter = 0;
+    for (int distance = 1; distance < x->nactive; distance *= 2, iter++) {
+        int last = (distance * 2 >= x->nactive);
+        int i = index_of(x->active, x->nactive, me);
+        ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BEFORE);
+        if (i >= 0) {
+            int pw = x->active[i ^ distance];
+            if (!ftar_is_dead(c, pw)) {
+                int out = (x->cur == WS_W) ? WS_T : WS_W;
+                const void *A = c->ws[x->cur];
+                const void *PA = ftar_buf(c, pw, peer_cur(x, pw));
+                int tag = (iter == 0) ? FDEV_TAG_STEP0 : FDEV_TAG_STEP;
+                if (last) run1(x, FDEV_REDUCE, c->ws[out], PA, A, FDEV_REMOTE_X, tag); /* dst = src + dst */
+                else run1(x, FDEV_REDUCE, c->ws[out], A, PA, FDEV_REMOTE_Y, tag);      /* src = dst + src */
+                ftar_drain(c);
+                x->cur = out;
+                publish_cur(x);
+            }
+            c->stats.steps++;
+        }
+        ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_AFTER);
+        ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BARRIER);
+        newf = ftar_sync(c); /* agree + barrier (:51-53) */
+        if (newf) {
+            int dd = rd_handler(x, newf, distance * 2);
+            distance = dd / 2;
+        }
+    }
+
+    /* ERRORS_ARE_FATAL barrier (:73-75), then the fan-out to inactive ranks (:78-89) */
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
+    ftar_sync_fatal(c);
+    if (x->ninactive > x->nactive) ftar_abort(c, 1); /* reference: inactive ranks wait forever */
+    int ii = index_of(x->inactive, x->ninactive, me);
+    if (ii >= 0) {
+        int from = x->active[ii];
+        run1(x, FDEV_COPY, dst, ftar_buf(c, from, peer_cur(x, from)), NULL, FDEV_REMOTE_X, FDEV_TAG_STEP);
+        c->stats.steps++;
+    } else {
+        run1(x, FDEV_COPY, dst, c->ws[x->cur], NULL, 0, FDEV_TAG_LOCAL);
+    }
+    ftar_drain(c);
+    ftar_sync_fatal(c); /* main's MPI_Barrier (:134); peers are done reading */
+    ftar_stats_end(c);
+    return FTAR_SUCCESS;
+}
+
+int ftar_recursive_doubling_host(const void *src, void *dst, size_t count, ftar_dtype dtype, ftar_op op,
+                                 ftar_comm *c)
+{
+    if (!c) return FTAR_ERR_ARG;
+    size_t es = ftar_esize(dtype);
+    if (es == 0) return FTAR_ERR_ARG;
+    size_t bytes = count * es;
+    if (bytes > c->hbytes) {
+        fdev_free(c->dev, c->hsend);
+        fdev_free(c->dev, c->hrecv);
+        c->hsend = c->hrecv = NULL;
+        if (fdev_alloc_plain(c->dev, bytes, &c->hsend) || fdev_alloc_plain(c->dev, bytes, &c->hrecv))
+            return FTAR_ERR_NOMEM;
+        c->hbytes = bytes;
+    }
+    if (bytes && fdev_h2d(c->dev, c->hsend, src, bytes)) return FTAR_ERR_DEVICE;
+    int rc = ftar_recursive_doubling(c->hsend, c->hrecv, count, dtype, op, c);
+    if (rc) return rc;
+    if (bytes && fdev_d2h(c->dev, dst, c->hrecv, bytes)) return FTAR_ERR_DEVICE;
+    return FTAR_SUCCESS;
+}

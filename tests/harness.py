@@ -1,0 +1,117 @@
+"""Multi-process runs of the C ABI under the ftrun launcher (test infrastructure).
+
+`run_probe` writes per-rank inputs, launches `ftrun -np P ftar_probe` against either the
+host-sim build (CPU tests of the host logic) or the product libftar.so (GPU parity), and
+collects per-rank outputs and statuses for comparison with the oracle.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import tempfile
+from dataclasses import dataclass
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOSTSIM = os.path.join(ROOT, "tests", "hostsim", "_build")
+PKG = os.path.join(ROOT, "fault-tolerant_amd")
+
+
+@dataclass
+class ProbeRun:
+    returncode: int
+    stdout: str
+    stderr: str
+    outputs: dict      # rank -> list of np arrays (one per iteration)
+    status: dict       # rank -> list of (rc, comm_rank, comm_size, recoveries)
+
+    @property
+    def aborted(self) -> bool:
+        return "MPI_ABORT" in self.stderr
+
+
+def kill_env(kills) -> str:
+    return ",".join(f"{r}:{ph}:{st}:{pt}" for (r, ph, st, pt) in kills)
+
+
+def run_probe(algo: str, inputs, kills=(), op: int = 0, iters: int = 1, backend: str = "hostsim",
+              timeout: int = 120, devmap: str | None = None, env_extra: dict | None = None) -> ProbeRun:
+    p = len(inputs)
+    dt = {np.dtype(np.int32): 0, np.dtype(np.float32): 1, np.dtype(np.int64): 2,
+          np.dtype(np.float64): 3}[inputs[0].dtype]
+    count = inputs[0].size
+    tmp = tempfile.mkdtemp(prefix="ftar_probe_")
+    try:
+        for r, x in enumerate(inputs):
+            np.ascontiguousarray(x).tofile(os.path.join(tmp, f"in_{r}.bin"))
+        if backend == "hostsim":
+            ftrun = os.path.join(HOSTSIM, "bin", "ftrun")
+            probe = os.path.join(HOSTSIM, "bin", "ftar_probe")
+        else:
+            ftrun = os.path.join(PKG, "bin", "ftrun")
+            probe = os.path.join(HOSTSIM, "gpu", "ftar_probe")
+        env = dict(os.environ)
+        tag = os.path.basename(tmp)
+        env.update(FTAR_PROBE_DIR=tmp, FTAR_PROBE_ALGO=algo, FTAR_PROBE_DTYPE=str(dt),
+                   FTAR_PROBE_OP=str(op), FTAR_PROBE_COUNT=str(count), FTAR_PROBE_ITERS=str(iters),
+                   FTAR_HOSTSIM_TAG=tag)
+        env.pop("FTAR_KILL", None)
+        if kills:
+            env["FTAR_KILL"] = kill_env(kills)
+        if env_extra:
+            env.update(env_extra)
+        cmd = [ftrun, "-np", str(p)]
+        if devmap:
+            cmd += ["--devmap", devmap]
+        cmd += [probe]
+        cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+        outs, stats = {}, {}
+        for r in range(p):
+            for it in range(iters):
+                f = os.path.join(tmp, f"out_{r}_{it}.bin")
+                s = os.path.join(tmp, f"status_{r}_{it}.txt")
+                if os.path.exists(f) and os.path.exists(s):
+                    outs.setdefault(r, []).append(np.fromfile(f, dtype=inputs[0].dtype))
+                    stats.setdefault(r, []).append(tuple(int(v) for v in open(s).read().split()))
+        return ProbeRun(cp.returncode, cp.stdout, cp.stderr, outs, stats)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+        for f in glob.glob(f"/dev/shm/ftarhs-{os.path.basename(tmp)}-*"):
+            try:
+                os.unlink(f)
+            except OSError:
+                pass
+
+
+def run_driver(which: str, nprocs: int, count: int, backend: str = "hostsim", kills=(),
+               env_extra: dict | None = None, timeout: int = 120):
+    """Run the drop-in src/<which>/main under ftrun and parse its stdout."""
+    if backend == "hostsim":
+        ftrun = os.path.join(HOSTSIM, "bin", "ftrun")
+        exe = os.path.join(HOSTSIM, "src", which, "main")
+    else:
+        ftrun = os.path.join(PKG, "bin", "ftrun")
+        exe = os.path.join(PKG, "src", which, "main")
+    env = dict(os.environ)
+    env["FTAR_HOSTSIM_TAG"] = f"drv{os.getpid()}"
+    env.pop("FTAR_KILL", None)
+    if kills:
+        env["FTAR_KILL"] = kill_env(kills)
+    if env_extra:
+        env.update(env_extra)
+    cp = subprocess.run([ftrun, "-np", str(nprocs), exe, str(count)], env=env, capture_output=True,
+                        text=True, timeout=timeout)
+    for f in glob.glob(f"/dev/shm/ftarhs-drv{os.getpid()}-*"):
+        try:
+            os.unlink(f)
+        except OSError:
+            pass
+    hello = {}
+    for line in cp.stdout.splitlines():
+        t = line.split()
+        if t and t[0] == "Hello":
+            hello[int(t[2])] = int(t[-1])
+    return cp, hello

@@ -1,0 +1,206 @@
+/*
+ * dev_host.c -- TEST-ONLY host implementation of the device layer (csrc/ftar_dev.h).
+ *
+ * Lets the CPU test suite run the product's real host logic -- control plane, agree,
+ * both schedules, both error handlers, the launcher, kill -9 injection -- as N real
+ * processes without a GPU.  "Device" allocations are POSIX shared-memory objects,
+ * the "IPC handle" is the object name, kernels are plain loops.  It is linked only
+ * into tests/hostsim/_build/libftar_hostsim.so, never into lib/libftar.so, and it is
+ * not used for any numerical parity claim about the HIP kernels.
+ */
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
+#include <fcntl.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "../../fault-tolerant_amd/csrc/ftar_dev.h"
+
+struct ftar_dev {
+    int device;
+    int profiling;
+    fdev_counters ctr;
+};
+
+#define MAXMAP 256
+static struct {
+    void *p;
+    size_t n;
+    char name[64];
+    int own;
+} g_map[MAXMAP];
+static int g_seq;
+static char g_err[256];
+
+const char *fdev_last_error(void) { return g_err; }
+
+int fdev_device_count(int *n)
+{
+    *n = 8;
+    return 0;
+}
+
+int fdev_open(int device, ftar_dev **out)
+{
+    ftar_dev *d = (ftar_dev *)calloc(1, sizeof(ftar_dev));
+    d->device = device;
+    *out = d;
+    return 0;
+}
+
+void fdev_close(ftar_dev *d) { free(d); }
+int fdev_device(const ftar_dev *d) { return d->device; }
+
+static int put_map(void *p, size_t n, const char *name, int own)
+{
+    for (int i = 0; i < MAXMAP; i++)
+        if (!g_map[i].p) {
+            g_map[i].p = p;
+            g_map[i].n = n;
+            g_map[i].own = own;
+            snprintf(g_map[i].name, sizeof(g_map[i].name), "%s", name);
+            return 0;
+        }
+    return -1;
+}
+
+int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
+{
+    char name[64];
+    const char *tag = getenv("FTAR_HOSTSIM_TAG");
+    snprintf(name, sizeof(name), "/ftarhs-%s-%d-%d", tag ? tag : "x", (int)getpid(), g_seq++);
+    int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) {
+        snprintf(g_err, sizeof(g_err), "shm_open %s failed", name);
+        return 101;
+    }
+    void *p = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return 102;
+    memset(handle, 0, FDEV_HANDLE_BYTES);
+    snprintf((char *)handle, FDEV_HANDLE_BYTES, "%s", name);
+    put_map(p, bytes, name, 1);
+    *ptr = p;
+    return 0;
+}
+
+int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr)
+{
+    *ptr = malloc(bytes ? bytes : 1);
+    return *ptr ? 0 : 102;
+}
+
+static int drop(void *ptr, int unlink_it)
+{
+    for (int i = 0; i < MAXMAP; i++)
+        if (g_map[i].p == ptr) {
+            munmap(ptr, g_map[i].n);
+            if (unlink_it && g_map[i].own) shm_unlink(g_map[i].name);
+            g_map[i].p = NULL;
+            return 0;
+        }
+    return -1;
+}
+
+int fdev_free(ftar_dev *d, void *ptr)
+{
+    if (!ptr) return 0;
+    if (drop(ptr, 1) != 0) free(ptr);
+    return 0;
+}
+
+int fdev_import(ftar_dev *d, const void *handle, void **ptr)
+{
+    char name[FDEV_HANDLE_BYTES + 1];
+    memcpy(name, handle, FDEV_HANDLE_BYTES);
+    name[FDEV_HANDLE_BYTES] = 0;
+    int fd = shm_open(name, O_RDWR, 0600);
+    if (fd < 0) {
+        snprintf(g_err, sizeof(g_err), "import %s failed", name);
+        return 101;
+    }
+    struct stat st;
+    fstat(fd, &st);
+    void *p = mmap(NULL, (size_t)st.st_size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return 101;
+    put_map(p, (size_t)st.st_size, name, 0);
+    *ptr = p;
+    return 0;
+}
+
+int fdev_unimport(ftar_dev *d, void *ptr) { return drop(ptr, 0) == 0 ? 0 : 101; }
+
+#define LOOP(T, UT)                                                                                         \
+    do {                                                                                                    \
+        T *o = (T *)s->out;                                                                                 \
+        const T *x = (const T *)s->x, *y = (const T *)s->y;                                                 \
+        for (size_t i = 0; i < s->n; i++) {                                                                 \
+            T a = x[i], b = y[i];                                                                           \
+            switch (op) {                                                                                   \
+            case 0: o[i] = (T)((UT)a + (UT)b); break;                                                       \
+            case 1: o[i] = (T)((UT)a * (UT)b); break;                                                       \
+            case 2: o[i] = (a > b) ? a : b; break;                                                          \
+            default: o[i] = (a < b) ? a : b; break;                                                         \
+            }                                                                                               \
+        }                                                                                                   \
+    } while (0)
+
+static size_t esz(int dt) { return (dt == 0 || dt == 1) ? 4 : 8; }
+
+int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    for (int k = 0; k < nseg; k++) {
+        const fdev_seg *s = &segs[k];
+        if (s->kind == FDEV_COPY) {
+            memmove(s->out, s->x, s->n * esz(dtype));
+            continue;
+        }
+        switch (dtype) {
+        case 0: LOOP(int32_t, uint32_t); break;
+        case 1: LOOP(float, float); break;
+        case 2: LOOP(int64_t, uint64_t); break;
+        default: LOOP(double, double); break;
+        }
+    }
+    d->ctr.launches[tag]++;
+    return 0;
+}
+
+int fdev_order_after(ftar_dev *d, void *s) { return 0; }
+
+int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
+{
+    if (poll) return poll(arg);
+    return 0;
+}
+
+int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t n)
+{
+    memcpy(dst, src, n);
+    return 0;
+}
+int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t n)
+{
+    memcpy(dst, src, n);
+    return 0;
+}
+
+void fdev_profiling(ftar_dev *d, int on) { d->profiling = on; }
+void fdev_counters_reset(ftar_dev *d) { memset(&d->ctr, 0, sizeof(d->ctr)); }
+void fdev_counters_get(ftar_dev *d, fdev_counters *out) { *out = d->ctr; }
+int fdev_set_reduce_variant(int v) { return 0; }
+
+int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream)
+{
+    fdev_seg s = {FDEV_REDUCE, 0, inout, inout, in, n};
+    ftar_dev d;
+    memset(&d, 0, sizeof(d));
+    return fdev_run(&d, dtype, op, &s, 1, 0);
+}
