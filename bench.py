@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""bench.py -- Allreduce GB/s (device-resident, float32 SUM) of the MI355X-native
+fault-tolerant Allreduce.
+
+  python bench.py [--gpus 1] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+N = 1: the single-GPU workload of BASELINE.json configs[1] -- the local-reduce HIP
+       kernel (MPI_Reduce_local, the per-step bucket reduction) on two 256 MiB float32
+       vectors.  One step = one kernel launch.  HBM-bound.
+N > 1: configs[3] -- fault-tolerant Rabenseifner Allreduce of a 256 MiB float32 vector
+       per rank, one rank per GPU, exchanges pulled over xGMI (weak scaling: every rank
+       contributes one 256 MiB vector).  One step = one Allreduce.  Recursive doubling
+       (configs[2]) and RCCL's all_reduce on the same buffers are reported beside it.
+
+value = (input vectors summed x bytes per vector) / time per step, whole job:
+        N=1: 2 x 256 MiB per launch; N>1: N x 256 MiB per Allreduce.
+Data are synthetic (uniform [-1, 1)), inputs resident in HBM before timing starts.
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+COUNT = 1 << 26              # 256 MiB of float32 per vector
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 76.8         # one xGMI link, one direction (153.6 GB/s bidirectional spec)
+METRIC = "Allreduce GB/s (device-resident, float32 SUM) at 1/2/4/8 MI355X"
+
+
+def load_package():
+    path = os.path.join(ROOT, "fault-tolerant_amd", "__init__.py")
+    spec = importlib.util.spec_from_file_location("ftar_amd", path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["ftar_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def pmc_traffic(name):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(name, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_local_reduce(min_seconds=10.0, max_passes=200):
+    """The oracle's MPI_Reduce_local restatement on the host (1 thread), same workload."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    rng = np.random.default_rng(1)
+    a = rng.random(COUNT, dtype=np.float32)
+    b = rng.random(COUNT, dtype=np.float32)
+    O.reduce_local(a, b)  # warm the pages
+    t0 = time.perf_counter()
+    passes = 0
+    while passes < max_passes and (time.perf_counter() - t0) < min_seconds:
+        O.reduce_local(a, b)
+        passes += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(2 * COUNT * 4 * passes / dt / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/ftar_oracle.c reduce_local, 2 x 256 MiB float32, {passes} passes "
+                      f"({dt:.1f} s), 1 host thread"}
+
+
+def single(args):
+    import torch
+    ftar = load_package()
+    ftar.lib()
+    torch.cuda.set_device(0)
+    g = torch.Generator(device="cuda").manual_seed(42)
+    x = torch.rand(args.count, device="cuda", generator=g) * 2 - 1
+    y = torch.rand(args.count, device="cuda", generator=g) * 2 - 1
+    ftar.set_reduce_variant(args.variant)
+    for _ in range(args.warmup):
+        ftar.reduce_local(x, y)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record()
+        ftar.reduce_local(x, y)  # launched on torch's current stream, the one the events see
+        e1.record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ms_step = (t1 - t0) * 1e3 / args.steps
+    k_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    S = args.count * 4
+    achieved = 3 * S / (k_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC, "value": round(2 * S / (ms_step * 1e-3) / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic uniform[-1,1), HBM-resident",
+        "config": {"workload": "configs[1]: local-reduce HIP kernel (MPI_Reduce_local), 2 x 256 MiB float32 SUM, "
+                               "1 MI355X", "count": args.count, "kernel_variant": args.variant},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("reduce_local_c2"),
+                     "kernel": "segment_kernel<float,SUM>", "algorithmic_bytes_per_launch": 3 * S,
+                     "kernel_ms": round(k_ms, 4)},
+    }
+    out["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_local_reduce()
+    print(json.dumps(out), flush=True)
+
+
+def multi(args):
+    import torch
+    import torch.distributed as dist
+    ftar = load_package()
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group(backend="nccl")
+    comm = ftar.Comm.from_env()
+    comm.set_profiling(True)
+    g = torch.Generator(device="cuda").manual_seed(1000 + rank)
+    x = torch.rand(args.count, device="cuda", generator=g) * 2 - 1
+    y = torch.empty_like(x)
+    S = args.count * 4
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step0 = 0.0
+        for _ in range(args.steps):
+            fn()
+            step0 += comm.last_stats().step0_kernel_ms
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        dist.barrier()
+        t = torch.tensor([t1 - t0, step0], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t[0].item() / args.steps, t[1].item() / args.steps
+
+    def raben():
+        rc = comm.allreduce_rabenseifner(x, y)
+        assert rc == 0, rc
+
+    def rd():
+        rc = comm.recursive_doubling(x, y)
+        assert rc == 0, rc
+
+    t_rb, k_rb = timed(raben)
+    # correctness spot check against RCCL on the same inputs (tolerance: fp32 tree order)
+    ref = x.clone()
+    dist.all_reduce(ref)
+    raben()
+    err = (y - ref).abs().max().item()
+    t_rd, k_rd = timed(rd)
+    z = x.clone()
+
+    def rccl():
+        dist.all_reduce(z)
+
+    t_nc, _ = timed(rccl)
+    L = world.bit_length() - 1
+    pow2 = (1 << L) == world
+    link_bytes_raben = (2.5 - 2.0 ** (1 - L)) * S if pow2 else None
+    t_roof = link_bytes_raben / (XGMI_LINK_GBS * 1e9) if link_bytes_raben else None
+    achieved = S / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None         # RS step-0 kernel pulls S bytes
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(world * S / t_rb / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_rb * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic uniform[-1,1), HBM-resident",
+            "config": {"workload": "configs[3]: fault-tolerant Rabenseifner Allreduce, 256 MiB float32 SUM per "
+                                   "rank, one rank per MI355X, pull exchanges over xGMI",
+                       "count": args.count, "parallelism": f"{world} ranks"},
+            "algbw_GBps": round(S / t_rb / 1e9, 2),
+            "schedule_link_roofline": {"bytes_per_rank_per_direction": link_bytes_raben, "link_GBps": XGMI_LINK_GBS,
+                                       "t_roof_ms": round(t_roof * 1e3, 3) if t_roof else None,
+                                       "frac": round(t_roof / t_rb, 4) if t_roof else None},
+            "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
+                         "peak": XGMI_LINK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / XGMI_LINK_GBS, 4) if achieved else None, "traffic": None,
+                         "kernel": "Raben RS step 0 (pull full partner vector, reduce half)",
+                         "algorithmic_bytes_per_launch": S, "kernel_ms": round(k_rb, 4)},
+            "rd": {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
+                   "step0_kernel_ms": round(k_rd, 4)},
+            "rccl_allreduce": {"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2)},
+            "max_abs_err_vs_rccl": err,
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    comm.finalize()
+    dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--count", type=int, default=COUNT)
+    ap.add_argument("--variant", type=int, default=0, help="local-reduce kernel: 0 register, 1 LDS-DMA")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        args.steps = args.steps or 20
+        args.warmup = args.warmup if args.warmup is not None else 3
+        multi(args)
+    else:
+        args.steps = args.steps or 200
+        args.warmup = args.warmup if args.warmup is not None else 10
+        single(args)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,216 @@
+"""Python mirror of the reference's Allreduce interface over libftar.so (ctypes).
+
+The product is the C ABI in include/ftar.h (lib/libftar.so: host-C schedules + HIP
+kernels for gfx950).  This module only binds it for Python callers (bench.py, the
+GPU tests): it keeps the reference's names and argument meaning
+
+    recursive_doubling(src, dst, count, dtype, op)        src/rd/header.h:29
+    allreduce_rabenseifner(sbuf, rbuf, count, dtype, op)  src/raben/header.h:14-15
+    reduce_local(in, inout, count, dtype, op)             MPI_Reduce_local call sites
+
+and raises if the native library is missing -- there is no Python or CPU fallback.
+Buffers are device pointers: ints, or torch tensors on the rank's GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libftar.so")
+
+INT32, FLOAT32, INT64, FLOAT64 = 0, 1, 2, 3
+SUM, PROD, MAX, MIN = 0, 1, 2, 3
+PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
+PT_BEFORE, PT_AFTER, PT_BARRIER = 0, 1, 2
+SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
+
+
+class FtarError(RuntimeError):
+    pass
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("steps", ctypes.c_int), ("recoveries", ctypes.c_int), ("comm_size_after", ctypes.c_int),
+                ("wall_s", ctypes.c_double), ("kernel_ms", ctypes.c_double),
+                ("step0_kernel_ms", ctypes.c_double), ("link_bytes", ctypes.c_double),
+                ("hbm_bytes", ctypes.c_double), ("kernels", ctypes.c_int)]
+
+
+class Kill(ctypes.Structure):
+    _fields_ = [("rank", ctypes.c_int), ("phase", ctypes.c_int), ("step", ctypes.c_int),
+                ("point", ctypes.c_int)]
+
+
+_lib = None
+
+
+def build(jobs: int = 8) -> str:
+    """Compile lib/libftar.so, the drivers and ftrun for gfx950 (make, hipcc)."""
+    subprocess.run(["make", "-s", "-C", HERE, f"-j{jobs}"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FtarError(f"{LIB_PATH} is not built: run `make -C {HERE}` (the HIP path has no fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    pp = ctypes.POINTER(vp)
+    sig = {
+        "ftar_init": ([pp], i),
+        "ftar_init_rank": ([pp, ctypes.c_char_p, i, i, i], i),
+        "ftar_finalize": ([vp], i),
+        "ftar_comm_rank": ([vp, ctypes.POINTER(i)], i),
+        "ftar_comm_size": ([vp, ctypes.POINTER(i)], i),
+        "ftar_world_rank": ([vp, ctypes.POINTER(i)], i),
+        "ftar_world_size": ([vp, ctypes.POINTER(i)], i),
+        "ftar_comm_device": ([vp, ctypes.POINTER(i)], i),
+        "ftar_barrier": ([vp], i),
+        "ftar_set_kills": ([vp, ctypes.POINTER(Kill), i], i),
+        "ftar_allreduce_rabenseifner": ([vp, vp, sz, i, i, vp], i),
+        "ftar_recursive_doubling": ([vp, vp, sz, i, i, vp], i),
+        "ftar_allreduce_rabenseifner_host": ([vp, vp, sz, i, i, vp], i),
+        "ftar_recursive_doubling_host": ([vp, vp, sz, i, i, vp], i),
+        "ftar_reduce_local": ([vp, vp, sz, i, i, vp], i),
+        "ftar_set_reduce_variant": ([i], i),
+        "ftar_comm_set_stream": ([vp, vp], i),
+        "ftar_last_stats": ([vp, ctypes.POINTER(Stats)], i),
+        "ftar_set_profiling": ([vp, i], i),
+        "ftar_version": ([], ctypes.c_char_p),
+    }
+    for name, (args, ret) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = ret
+    L.ftar_abort.argtypes = [vp, i]
+    L.ftar_abort.restype = None
+    _lib = L
+    return L
+
+
+def _dtype_of(t) -> int:
+    import torch
+    m = {torch.int32: INT32, torch.float32: FLOAT32, torch.int64: INT64, torch.float64: FLOAT64}
+    if t.dtype not in m:
+        raise FtarError(f"unsupported dtype {t.dtype}")
+    return m[t.dtype]
+
+
+def _ptr(x):
+    if isinstance(x, int):
+        return x
+    if not x.is_cuda or not x.is_contiguous():
+        raise FtarError("buffers must be contiguous device tensors")
+    return x.data_ptr()
+
+
+def _check(rc: int, what: str):
+    if rc != SUCCESS:
+        raise FtarError(f"{what} failed with code {rc}")
+
+
+def reduce_local(inp, inout, count=None, dtype=None, op: int = SUM, stream=None):
+    """MPI_Reduce_local(in, inout): inout = inout <op> in on the GPU (asynchronous on
+    `stream`, default the current torch stream)."""
+    if count is None:
+        count = inout.numel()
+    if dtype is None:
+        dtype = _dtype_of(inout)
+    if stream is None and not isinstance(inout, int):
+        import torch
+        stream = torch.cuda.current_stream(inout.device).cuda_stream
+    _check(lib().ftar_reduce_local(_ptr(inp), _ptr(inout), count, dtype, op, stream or None), "ftar_reduce_local")
+
+
+def set_reduce_variant(v: int):
+    _check(lib().ftar_set_reduce_variant(v), "ftar_set_reduce_variant")
+
+
+class Comm:
+    """An ftar communicator (one per rank process)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def from_env(cls):
+        h = ctypes.c_void_p()
+        _check(lib().ftar_init(ctypes.byref(h)), "ftar_init")
+        return cls(h)
+
+    @classmethod
+    def init_rank(cls, job: str, rank: int, size: int, device: int):
+        h = ctypes.c_void_p()
+        _check(lib().ftar_init_rank(ctypes.byref(h), job.encode(), rank, size, device), "ftar_init_rank")
+        return cls(h)
+
+    def _q(self, fn):
+        v = ctypes.c_int()
+        _check(fn(self._h, ctypes.byref(v)), fn.__name__)
+        return v.value
+
+    @property
+    def rank(self):
+        return self._q(lib().ftar_comm_rank)
+
+    @property
+    def size(self):
+        return self._q(lib().ftar_comm_size)
+
+    @property
+    def world_rank(self):
+        return self._q(lib().ftar_world_rank)
+
+    @property
+    def world_size(self):
+        return self._q(lib().ftar_world_size)
+
+    @property
+    def device(self):
+        return self._q(lib().ftar_comm_device)
+
+    def barrier(self):
+        _check(lib().ftar_barrier(self._h), "ftar_barrier")
+
+    def set_stream(self, stream):
+        _check(lib().ftar_comm_set_stream(self._h, stream), "ftar_comm_set_stream")
+
+    def set_profiling(self, on: bool):
+        _check(lib().ftar_set_profiling(self._h, int(on)), "ftar_set_profiling")
+
+    def set_kills(self, kills):
+        arr = (Kill * max(1, len(kills)))(*[Kill(*k) for k in kills])
+        _check(lib().ftar_set_kills(self._h, arr, len(kills)), "ftar_set_kills")
+
+    def last_stats(self) -> Stats:
+        s = Stats()
+        _check(lib().ftar_last_stats(self._h, ctypes.byref(s)), "ftar_last_stats")
+        return s
+
+    def allreduce_rabenseifner(self, sbuf, rbuf, count=None, dtype=None, op: int = SUM) -> int:
+        if count is None:
+            count = rbuf.numel()
+        if dtype is None:
+            dtype = _dtype_of(rbuf)
+        return lib().ftar_allreduce_rabenseifner(_ptr(sbuf), _ptr(rbuf), count, dtype, op, self._h)
+
+    def recursive_doubling(self, src, dst, count=None, dtype=None, op: int = SUM) -> int:
+        if count is None:
+            count = dst.numel()
+        if dtype is None:
+            dtype = _dtype_of(dst)
+        return lib().ftar_recursive_doubling(_ptr(src), _ptr(dst), count, dtype, op, self._h)
+
+    def finalize(self):
+        if self._h:
+            _check(lib().ftar_finalize(self._h), "ftar_finalize")
+            self._h = None
+
+
+def version() -> str:
+    return lib().ftar_version().decode()

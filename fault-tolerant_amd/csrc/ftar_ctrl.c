@@ -70,6 +70,7 @@ int ftar_ctrl_create(ftar_job *job, const char *name, int size)
     job->shm->magic = FTAR_SHM_MAGIC;
     job->shm->version = FTAR_SHM_VERSION;
     job->shm->size = size;
+    for (int i = 0; i < FTAR_DECISIONS; i++) atomic_store(&job->shm->decision[i], FTAR_UNDECIDED);
     atomic_store_explicit(&job->shm->ready, 1, memory_order_release);
     job->size = size;
     job->rank = -1;
@@ -226,14 +227,14 @@ uint64_t ftar_ctrl_agree(ftar_job *job, uint64_t members)
     for (unsigned long it = 0;; it++) {
         if (atomic_load_explicit(&S->abort_flag, memory_order_acquire)) exit_aborted(job);
         uint64_t w = atomic_load_explicit(&S->decision[idx], memory_order_acquire);
-        if (w & FTAR_DECIDED) return w & ~FTAR_DECIDED;
+        if (w != FTAR_UNDECIDED) return w;
         if (round_complete(job, members, seq, t0)) {
-            uint64_t snap = ftar_ctrl_failed(job) & members & ~FTAR_DECIDED;
-            uint64_t expect = 0;
-            if (atomic_compare_exchange_strong_explicit(&S->decision[idx], &expect, snap | FTAR_DECIDED,
+            uint64_t snap = ftar_ctrl_failed(job) & members;
+            uint64_t expect = FTAR_UNDECIDED;
+            if (atomic_compare_exchange_strong_explicit(&S->decision[idx], &expect, snap,
                                                         memory_order_acq_rel, memory_order_acquire)) {
                 /* every live member has read round seq-1 before arriving here: recycle it */
-                atomic_store_explicit(&S->decision[(seq - 1) % FTAR_DECISIONS], 0, memory_order_release);
+                atomic_store_explicit(&S->decision[(seq - 1) % FTAR_DECISIONS], FTAR_UNDECIDED, memory_order_release);
             }
             continue;
         }

@@ -33,7 +33,8 @@
 #define FTAR_SLOT_RUNNING 2
 #define FTAR_SLOT_FINALIZED 3
 
-#define FTAR_DECIDED (1ull << 63)
+/* an undecided ring entry: never a valid snapshot, which always omits the decider */
+#define FTAR_UNDECIDED (~0ull)
 
 typedef struct {
     pthread_mutex_t alive;          /* robust + pshared, locked by the owner while alive */

@@ -88,7 +88,7 @@ typedef struct {
     int point; /* FTAR_PT_* */
 } ftar_kill;
 
-#define FTAR_MAX_RANKS 63 /* the agree decision word holds one bit per rank + a decided bit */
+#define FTAR_MAX_RANKS 64 /* failure sets are one 64-bit word, one bit per original rank */
 #define FTAR_MAX_KILLS 16
 
 /* ---- communicator -------------------------------------------------------- */

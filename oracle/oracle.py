@@ -21,7 +21,7 @@ SUM, PROD, MAX, MIN = 0, 1, 2, 3
 PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
 PT_BEFORE, PT_AFTER, PT_BARRIER = 0, 1, 2
 OK, DEAD, ABORTED = 0, 1, 2
-MAX_RANKS = 63
+MAX_RANKS = 64
 
 NP_DTYPE = {INT32: np.int32, FLOAT32: np.float32, INT64: np.int64, FLOAT64: np.float64}
 DTYPE_OF = {np.dtype(v): k for k, v in NP_DTYPE.items()}

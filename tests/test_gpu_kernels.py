@@ -1,0 +1,113 @@
+"""GPU parity of the local-reduce kernel (MPI_Reduce_local) against the CPU oracle.
+
+Bar: bit-exact for every dtype/op on the same inputs (one IEEE op per element for
+floats; two's-complement wrap for ints).  Sizes cover empty, ragged, unaligned heads
+and tails, non-co-aligned pointers (scalar path) and the full 256 MiB C2 vector.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+NP = {0: np.int32, 1: np.float32, 2: np.int64, 3: np.float64}
+UINT = {4: np.uint32, 8: np.uint64}
+
+
+def _inputs(dt, n, seed, specials=False):
+    rng = np.random.default_rng(seed)
+    t = NP[dt]
+    if np.dtype(t).kind == "f":
+        a = (rng.standard_normal(n) * 100).astype(t)
+        b = (rng.standard_normal(n) * 100).astype(t)
+        if specials and n >= 16:
+            sp = np.array([0.0, -0.0, np.inf, -np.inf, 1e-40, -1e-40, 3.4e38, -3.4e38], dtype=t)
+            a[:8] = sp
+            b[8:16] = sp
+    else:
+        info = np.iinfo(t)
+        a = rng.integers(info.min, info.max, n, dtype=t, endpoint=True)
+        b = rng.integers(info.min, info.max, n, dtype=t, endpoint=True)
+    return a, b
+
+
+def _same_bits(x, y):
+    u = UINT[x.dtype.itemsize]
+    return np.array_equal(x.view(u), y.view(u))
+
+
+def _to_dev(a):
+    import torch
+    return torch.from_numpy(a.copy()).cuda()
+
+
+@pytest.mark.parametrize("dt", [0, 1, 2, 3])
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+@pytest.mark.parametrize("n", [0, 1, 3, 17, 1000, 65537, 1 << 20])
+def test_reduce_local_bit_exact(ftar, oracle, dt, op, n):
+    import torch
+    a, b = _inputs(dt, n, seed=n * 7 + op, specials=(op >= 2 or n > 100))
+    x, y = _to_dev(a), _to_dev(b)
+    ftar.reduce_local(x, y, op=op)  # y = y <op> x
+    torch.cuda.synchronize()
+    want = b.copy()
+    oracle.reduce_local(a, want, op)
+    assert _same_bits(y.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("off_in,off_io", [(1, 1), (3, 3), (1, 2), (0, 3), (2, 0)])
+def test_reduce_local_unaligned(ftar, oracle, off_in, off_io):
+    """Heads/tails (co-aligned offsets) and the scalar path (different alignments)."""
+    import torch
+    n = 100003
+    a, b = _inputs(1, n + 8, seed=11)
+    x, y = _to_dev(a), _to_dev(b)
+    ftar.reduce_local(x[off_in:off_in + n], y[off_io:off_io + n], count=n, dtype=1, op=0)
+    torch.cuda.synchronize()
+    want = b.copy()
+    part = want[off_io:off_io + n].copy()
+    oracle.reduce_local(a[off_in:off_in + n].copy(), part, 0)
+    want[off_io:off_io + n] = part
+    assert _same_bits(y.cpu().numpy(), want)  # untouched outside the window too
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_reduce_local_c2_full_size(ftar, variant):
+    """C2: two 256 MiB float32 vectors; property check against torch's own fp32 add
+    (one IEEE add per element, so bit-identical)."""
+    import torch
+    n = 1 << 26
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    want = y + x
+    ftar.set_reduce_variant(variant)
+    try:
+        ftar.reduce_local(x, y, op=0)
+        torch.cuda.synchronize()
+    finally:
+        ftar.set_reduce_variant(0)
+    assert torch.equal(y.view(torch.int32), want.view(torch.int32))
+
+
+@pytest.mark.parametrize("dt", [0, 1, 2, 3])
+def test_reduce_local_lds_variant_bit_exact(ftar, oracle, dt):
+    import torch
+    n = (1 << 20) + 256  # multiple of 16 bytes for every dtype
+    a, b = _inputs(dt, n, seed=dt)
+    x, y = _to_dev(a), _to_dev(b)
+    ftar.set_reduce_variant(1)
+    try:
+        ftar.reduce_local(x, y, op=0)
+        torch.cuda.synchronize()
+    finally:
+        ftar.set_reduce_variant(0)
+    want = b.copy()
+    oracle.reduce_local(a, want, 0)
+    assert _same_bits(y.cpu().numpy(), want)
+
+
+def test_reduce_local_rejects_bad_args(ftar):
+    import torch
+    x = torch.zeros(16, device="cuda")
+    with pytest.raises(ftar.FtarError):
+        ftar.reduce_local(x, x, dtype=9)

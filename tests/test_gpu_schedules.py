@@ -1,0 +1,113 @@
+"""GPU parity of the two fault-tolerant schedules against the CPU oracle.
+
+Each case launches P rank processes with ftrun (all on GPU 0 of the one-GPU test box:
+the IPC peer mappings, pull kernels, control plane and recovery run exactly as on 8
+GPUs, only the fabric is local HBM) and compares every survivor's output bit for bit
+with the oracle's global simulation of the reference on the same inputs.  Kill cases
+use deterministic injection (FTAR_KILL) and check both the outcome class (recover vs
+MPI_Abort) and the data.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import harness as H
+
+pytestmark = pytest.mark.gpu
+
+ALL_ON_GPU0 = ",".join(["0"] * 16)
+
+
+def _check(oracle_fn, algo, inputs, kills=(), op=0, iters=1):
+    o = oracle_fn(inputs, kills, op=op)
+    r = H.run_probe(algo, inputs, kills, op=op, iters=iters, backend="gpu", devmap=ALL_ON_GPU0, timeout=300)
+    u = {4: np.uint32, 8: np.uint64}[inputs[0].dtype.itemsize]
+    if o.aborted:
+        assert r.aborted, r.stderr[-2000:]
+        assert not r.outputs
+        return o, r
+    assert not r.aborted, r.stderr[-2000:]
+    for w, st in enumerate(o.status):
+        if st == 0:
+            assert w in r.outputs, (w, r.stderr[-2000:])
+            got = r.outputs[w][0]
+            assert np.array_equal(got.view(u), o.outputs[w].view(u)), (w, algo, kills)
+        else:
+            assert w not in r.outputs
+    return o, r
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 5, 8, 9])
+def test_schedule_nofault_float32(oracle, algo, p):
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    _check(fn, algo, oracle.random_inputs(p, 100003, seed=p))
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("dtype", [np.int32, np.int64, np.float64])
+def test_schedule_nofault_dtypes(oracle, algo, dtype):
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    _check(fn, algo, oracle.random_inputs(6, 4099, seed=3, dtype=dtype))
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+def test_schedule_reference_inputs_checksum(oracle, algo):
+    """The reference drivers' case: buffer[i] = rank, int32 SUM, checksum closed form."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    o, r = _check(fn, algo, oracle.rank_inputs(8, 16384))
+    for w in range(8):
+        assert oracle.checksum17(r.outputs[w][0]) == oracle.expected_checksum(8, 16384)
+
+
+@pytest.mark.parametrize("kill", [(5, 1, 1, 2), (5, 1, 2, 2), (1, 1, 1, 2), (4, 2, 1, 2), (3, 2, 0, 2),
+                                  (6, 1, 0, 2), (2, 2, 2, 2), (5, 1, 1, 0), (7, 2, 1, 1)])
+def test_raben_single_kill_p9(oracle, kill):
+    """C5 layout: 9 ranks = 8 + one idle spare (rank 1); recoverable and aborting cases."""
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(9, 65536 + 5, seed=9), [kill])
+
+
+@pytest.mark.parametrize("kill", [(3, 1, 1, 2), (0, 1, 2, 2), (2, 1, 0, 2), (6, 1, 1, 0), (5, 1, 2, 1)])
+def test_rd_single_kill(oracle, kill):
+    p = 8 if kill[0] < 8 else 9
+    _check(oracle.recursive_doubling, "rd", oracle.random_inputs(p, 65536 + 3, seed=4), [kill])
+
+
+def test_rd_spare_branch_p6(oracle):
+    """Non power of two: an active death is repaired by waking the spare (deviation from
+    the reference, which spins forever at rd/errhandler.c:100-111)."""
+    _check(oracle.recursive_doubling, "rd", oracle.random_inputs(6, 10007, seed=6), [(1, 1, 1, 2)])
+
+
+def test_raben_two_failures_p11(oracle):
+    """Two sequential recoveries (rem = 3 idle ranks)."""
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(11, 30011, seed=11), [(4, 1, 1, 2), (9, 2, 1, 2)])
+
+
+def test_repeated_calls_after_recovery(oracle):
+    """The comm is re-targeted by a recovery and the next call runs on the survivors."""
+    inputs = oracle.random_inputs(5, 20000, seed=2)
+    r = H.run_probe("raben", inputs, [(3, 1, 1, 2)], iters=3, backend="gpu", devmap=ALL_ON_GPU0)
+    o1 = oracle.rabenseifner(inputs, [(3, 1, 1, 2)])
+    assert not r.aborted, r.stderr[-2000:]
+    survivors = [w for w in range(5) if w != 3]
+    for w in survivors:
+        assert np.array_equal(r.outputs[w][0].view(np.uint32), o1.outputs[w].view(np.uint32))
+        assert r.status[w][1][2] == 4  # comm size after the recovery
+    # later calls: a 4-rank comm in the re-targeted order; the sum is over survivors
+    order = o1.order_after
+    o2 = oracle.rabenseifner([inputs[w] for w in order])
+    for i, w in enumerate(order):
+        for it in (1, 2):
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o2.outputs[i].view(np.uint32))
+
+
+def test_driver_checksums(oracle):
+    """The drop-in src/raben/main and src/rd/main print the reference's lines."""
+    for which in ("raben", "rd"):
+        cp, hello = H.run_driver(which, 4, 100000, backend="gpu", env_extra={"FTAR_DEVMAP": ALL_ON_GPU0})
+        assert cp.returncode == 0, cp.stderr[-2000:]
+        assert sorted(hello) == [0, 1, 2, 3]
+        assert set(hello.values()) == {oracle.expected_checksum(4, 100000)}
+        assert "P: 4" in cp.stdout and "Size: 100000" in cp.stdout and "Time:" in cp.stdout

@@ -1,0 +1,42 @@
+#!/bin/bash
+# GPU-box validation script (run from the repo root via gpurun).  Every GPU step has
+# its own time limit; a fault/abort/timeout stops the script, test failures do not.
+set -u
+OUT=${OUT:-gpurun_out}
+mkdir -p "$OUT"
+ROOT=$(pwd)
+stop_on_fault() { # $1 = rc, $2 = step
+    local rc=$1
+    echo "$2 rc=$rc"
+    if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "STOP after $2 (rc=$rc)"; exit "$rc"; fi
+}
+STEPS=${STEPS:-smoke,pytest,bench,prof}
+if [[ $STEPS == *smoke* ]]; then
+  timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+  rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; [ $rc -eq 0 ] || exit $rc
+fi
+if [[ $STEPS == *pytest* ]]; then
+  timeout -k 10 ${PYTEST_TIMEOUT:-1200} python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+  rc=$?; tail -15 "$OUT/pytest_gpu.log"; stop_on_fault $rc pytest
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+  rc=$?; cat "$OUT/bench.json"; stop_on_fault $rc bench
+  timeout -k 10 300 python bench.py --variant 1 --no-cpu-baseline > "$OUT/bench_v1.json" 2>> "$OUT/bench.err"
+  rc=$?; cat "$OUT/bench_v1.json"; stop_on_fault $rc bench_v1
+fi
+if [[ $STEPS == *prof* ]]; then
+  export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof_c2" -o c2 --output-format csv -- \
+      python3 "$ROOT/bench.py" --steps 100 --warmup 5 --no-cpu-baseline > "$OUT/prof_c2.log" 2>&1
+  rc=$?; tail -3 "$OUT/prof_c2.log"; stop_on_fault $rc prof_c2
+fi
+if [[ $STEPS == *pmc* ]]; then
+  export TMPDIR=/tmp
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $ctr -d "$ROOT/$OUT/pmc_$ctr" -o pmc --output-format csv -- \
+        python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline > "$OUT/pmc_$ctr.log" 2>&1
+    rc=$?; tail -2 "$OUT/pmc_$ctr.log"; stop_on_fault $rc pmc_$ctr
+  done
+fi
+echo ALLDONE
