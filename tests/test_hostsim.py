@@ -1,0 +1,175 @@
+"""CPU tests of the product's host logic, as real multi-process jobs.
+
+The product's host C (control plane, agree/barrier, both schedules, both error
+handlers, the ftrun launcher and the drop-in drivers) is linked against a host-memory
+device layer (tests/hostsim/dev_host.c, test-only) so every rank is a real process,
+failures are real SIGKILLs detected through the robust-mutex failure detector, and the
+outcomes are compared with the oracle's simulation of the reference.
+"""
+import os
+import random
+import signal
+import subprocess
+import time
+
+import numpy as np
+import pytest
+
+import harness as H
+
+
+def _cmp(oracle_fn, algo, inputs, kills=(), op=0):
+    o = oracle_fn(inputs, kills, op=op)
+    r = H.run_probe(algo, inputs, kills, op=op, backend="hostsim", timeout=120)
+    u = {4: np.uint32, 8: np.uint64}[inputs[0].dtype.itemsize]
+    if o.aborted:
+        assert r.aborted and not r.outputs, (kills, r.stderr[-1000:])
+        return o, r
+    assert not r.aborted, (kills, r.stderr[-1000:])
+    for w, st in enumerate(o.status):
+        if st == 0:
+            assert np.array_equal(r.outputs[w][0].view(u), o.outputs[w].view(u)), (algo, kills, w)
+        else:
+            assert w not in r.outputs
+    return o, r
+
+
+def _fn(oracle, algo):
+    return oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 16, 17])
+def test_nofault_parity(hostsim, oracle, algo, p):
+    _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 1031, seed=p))
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("dtype,op", [(np.int32, 0), (np.int64, 1), (np.float64, 2), (np.float32, 3)])
+def test_nofault_dtypes_ops(hostsim, oracle, algo, dtype, op):
+    _cmp(_fn(oracle, algo), algo, oracle.random_inputs(6, 333, seed=2, dtype=dtype), op=op)
+
+
+@pytest.mark.parametrize("algo,p", [("raben", 5), ("raben", 9), ("raben", 8), ("rd", 4), ("rd", 6), ("rd", 8),
+                                    ("rd", 9)])
+def test_single_kill_sweep(hostsim, oracle, algo, p):
+    """Every victim x phase x step x point the schedule reaches: same outcome class
+    (recover / abort) and bit-identical survivor results."""
+    ins = oracle.random_inputs(p, 257, seed=p)
+    phases = [0, 1, 2, 3] if algo == "raben" else [0, 1, 3]
+    fn = _fn(oracle, algo)
+    n = 0
+    for v in range(p):
+        for ph in phases:
+            for st in range(4):
+                for pt in range(3):
+                    ks = [(v, ph, st, pt)]
+                    if fn(ins, ks).status[v] != oracle.DEAD:
+                        continue
+                    _cmp(fn, algo, ins, ks)
+                    n += 1
+    assert n > 0
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_multi_kill_random(hostsim, oracle, seed):
+    rng = random.Random(seed)
+    algo = rng.choice(["raben", "rd"])
+    p = rng.choice([6, 7, 9, 11, 13, 17])
+    nk = rng.choice([1, 2, 3])
+    victims = rng.sample(range(p), nk)
+    kills = [(v, rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(4), rng.randrange(3)) for v in victims]
+    _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 511, seed=seed), kills)
+
+
+def test_repeated_calls_and_retargeted_comm(hostsim, oracle):
+    inputs = oracle.random_inputs(5, 2000, seed=2)
+    kills = [(3, 1, 1, 2)]
+    r = H.run_probe("raben", inputs, kills, iters=3, backend="hostsim")
+    o1 = oracle.rabenseifner(inputs, kills)
+    assert not r.aborted
+    order = o1.order_after
+    o2 = oracle.rabenseifner([inputs[w] for w in order])
+    for i, w in enumerate(order):
+        assert np.array_equal(r.outputs[w][0].view(np.uint32), o1.outputs[w].view(np.uint32))
+        assert r.status[w][0][1:] == (i, 4, 1)      # comm rank, size, recoveries after the call
+        for it in (1, 2):
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o2.outputs[i].view(np.uint32))
+
+
+def test_rd_after_raben_recovery(hostsim, oracle):
+    """RD after a Raben recovery runs on the re-targeted comm order."""
+    inputs = oracle.random_inputs(9, 777, seed=5)
+    kills = [(4, 1, 2, 2)]
+    o1 = oracle.rabenseifner(inputs, kills)
+    assert not o1.aborted
+    r = H.run_probe("raben", inputs, kills, iters=2, backend="hostsim")
+    assert not r.aborted
+    for w in o1.order_after:
+        assert np.array_equal(r.outputs[w][0].view(np.uint32), o1.outputs[w].view(np.uint32))
+
+
+def test_zero_count_returns_mpi_err_unknown(hostsim, oracle):
+    r = H.run_probe("raben", [np.zeros(0, np.float32)] * 3, backend="hostsim")
+    assert all(r.status[w][0][0] == 14 for w in range(3))
+
+
+@pytest.mark.parametrize("which", ["raben", "rd"])
+@pytest.mark.parametrize("n", [4, 5, 6, 8, 9])
+def test_drivers_print_reference_lines(hostsim, oracle, which, n):
+    cp, hello = H.run_driver(which, n, 16384)
+    assert cp.returncode == 0, cp.stderr
+    assert sorted(hello) == list(range(n))
+    assert set(hello.values()) == {oracle.expected_checksum(n, 16384)}
+    lines = cp.stdout.splitlines()
+    assert lines.count(f"P: {n}") == n and lines.count("Size: 16384") == n
+    assert sum(1 for l in lines if l.startswith("Time: ")) == n
+    assert all(l.strip() for l in lines)  # check_fault.py indexes line[0]: no empty lines
+
+
+def test_driver_float32_mode(hostsim, oracle):
+    cp, hello = H.run_driver("raben", 5, 1000, env_extra={"FTAR_DTYPE": "float32"})
+    assert set(hello.values()) == {oracle.expected_checksum(5, 1000)}
+
+
+def test_driver_recovers_and_aborts_like_reference(hostsim, oracle):
+    # Raben N=9: a kill in a middle reduce-scatter step is recovered by the idle rank
+    cp, hello = H.run_driver("raben", 9, 5000, kills=[(5, 1, 1, 0)])
+    assert cp.returncode == 0 and sorted(hello) == [0, 1, 2, 3, 4, 6, 7, 8]
+    assert set(hello.values()) == {oracle.expected_checksum(9, 5000)}  # includes the dead rank's data
+    # Raben N=8: no idle rank -> MPI_Abort, nobody prints Hello
+    cp, hello = H.run_driver("raben", 8, 5000, kills=[(5, 1, 1, 0)])
+    assert cp.returncode != 0 and not hello
+    assert any(l.split() and l.split()[0] == "MPI_ABORT" for l in cp.stderr.splitlines())
+
+
+def _children(pid):
+    out = subprocess.run(["ps", "-o", "pid=,stat=,args=", "--ppid", str(pid)], capture_output=True, text=True).stdout
+    return [l.split(None, 2) for l in out.splitlines() if l.strip()]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_external_kill_never_wrong(hostsim, oracle, seed):
+    """kill_procs.sh-style: SIGKILL one running rank at a random time.  The job either
+    recovers with the right checksum (dead rank's data included) or aborts cleanly; it
+    never prints a wrong result and never hangs."""
+    rng = random.Random(seed)
+    n = rng.choice([5, 9])
+    count = 1 << 22
+    env = dict(os.environ, FTAR_HOSTSIM_TAG=f"ext{seed}")
+    env.pop("FTAR_KILL", None)
+    p = subprocess.Popen([os.path.join(hostsim, "bin", "ftrun"), "-np", str(n),
+                          os.path.join(hostsim, "src", "raben", "main"), str(count)],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    time.sleep(rng.uniform(0.05, 0.4))
+    kids = [c for c in _children(p.pid) if "main" in c[2]]
+    if kids:
+        victim = int(rng.choice(kids)[0])
+        os.kill(victim, signal.SIGKILL)
+    out, err = p.communicate(timeout=120)
+    hello = {int(l.split()[2]): int(l.split()[-1]) for l in out.splitlines() if l.startswith("Hello")}
+    aborted = any(l.split() and l.split()[0] == "MPI_ABORT" for l in err.splitlines())
+    assert aborted or set(hello.values()) <= {oracle.expected_checksum(n, count)}
+    if not aborted:
+        assert len(hello) >= n - 1
+    subprocess.run(f"rm -f /dev/shm/ftarhs-ext{seed}-*", shell=True)
