@@ -44,6 +44,15 @@ size_t esize_of(int dtype)
     }
 }
 
+// Streaming kernels: up to 32 workgroups of 256 threads per CU in the grid (8 resident,
+// the rest queued) -- the best grid of the C2 sweep (profiles/, tools/reduce_sweep.hip).
+unsigned blocks_per_cu()
+{
+    const char *e = getenv("FTAR_BLOCKS_PER_CU");
+    int v = e ? atoi(e) : 32;
+    return (unsigned)(v < 1 ? 1 : v > 256 ? 256 : v);
+}
+
 struct Pending {
     hipEvent_t start, stop;
     int tag;
@@ -87,8 +96,7 @@ int fdev_open(int device, ftar_dev **out)
     memset(&d->ctr, 0, sizeof(d->ctr));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
-    // 8 resident 256-thread workgroups per CU (32 waves/CU) for the streaming kernels
-    d->max_blocks = (unsigned)prop.multiProcessorCount * 8u;
+    d->max_blocks = (unsigned)prop.multiProcessorCount * blocks_per_cu();
     if (d->max_blocks == 0) d->max_blocks = 2048;
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     // Peer access to every other GPU of the node: the exchanges read peers' HBM.
@@ -293,7 +301,7 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
     static unsigned cached_blocks = 2048;
     if (cached_dev != dev) {
         HIPCHK(hipGetDeviceProperties(&prop, dev));
-        cached_blocks = (unsigned)prop.multiProcessorCount * 8u;
+        cached_blocks = (unsigned)prop.multiProcessorCount * blocks_per_cu();
         cached_dev = dev;
     }
     hipStream_t s = (hipStream_t)stream;

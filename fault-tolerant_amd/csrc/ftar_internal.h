@@ -48,6 +48,7 @@ struct ftar_comm {
     int profiling;
     ftar_stats stats;
     int verbose;
+    double step_delay_s; /* FTAR_STEP_DELAY_MS: stretch every tolerant barrier (harness knob) */
 };
 
 size_t ftar_esize(int dtype);

@@ -4,9 +4,10 @@
 // the operands, no reuse, no MFMA.  What matters on MI355X:
 //   * 16-byte lanes (global_load_dwordx4 / global_store_dwordx4): 1 KiB per wave
 //     instruction, the widest coalesced access;
-//   * enough bytes in flight: each lane issues UNROLL independent 16-byte loads per
-//     operand before it consumes any (128 B per lane for a reduce), and the grid holds
-//     up to 8 workgroups of 4 waves per CU (32 waves/CU);
+//   * enough bytes in flight: each lane issues UNROLL independent 16-byte non-temporal
+//     loads per operand before it consumes any (128 B per lane for a reduce); the grid
+//     has up to 32 workgroups of 4 waves per CU (8 resident = 32 waves/CU, the rest
+//     queued), the best grid of the C2 sweep;
 //   * one launch handles up to FDEV_MAX_KSEGS independent segments (e.g. Raben's
 //     step 0: reduce half the window + copy the other half of the partner's vector),
 //     blocks are split between segments in proportion to their bytes and each wave
@@ -66,6 +67,17 @@ __device__ __forceinline__ uint4 apply16(uint4 a, uint4 b)
 constexpr int kBlock = 256;
 constexpr int kUnroll = 4;
 
+// Streaming operands are read once: non-temporal loads (global_load_dwordx4 ... nt) keep
+// them from displacing useful lines and measured 6.36 TB/s against 5.2-5.5 TB/s for
+// plain loads on the C2 reduce (tools/reduce_sweep.hip, profiles/).  Stores stay plain:
+// non-temporal stores were slower in every configuration of that sweep.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldnt(const uint4 *p)
+{
+    v4u v = __builtin_nontemporal_load((const v4u *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ int find_segment(const KSegList &L)
 {
     // blockIdx is wave-uniform; readfirstlane keeps the search in SGPRs.
@@ -89,22 +101,22 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk)
         for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
             uint4 a[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; u++) a[u] = X[i + u * stride];
+            for (int u = 0; u < kUnroll; u++) a[u] = ldnt(X + i + u * stride);
 #pragma unroll
             for (int u = 0; u < kUnroll; u++) O[i + u * stride] = a[u];
         }
-        for (; i < nv; i += stride) O[i] = X[i];
+        for (; i < nv; i += stride) O[i] = ldnt(X + i);
     } else {
         for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
             uint4 a[kUnroll], c[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; u++) a[u] = X[i + u * stride];
+            for (int u = 0; u < kUnroll; u++) a[u] = ldnt(X + i + u * stride);
 #pragma unroll
-            for (int u = 0; u < kUnroll; u++) c[u] = Y[i + u * stride];
+            for (int u = 0; u < kUnroll; u++) c[u] = ldnt(Y + i + u * stride);
 #pragma unroll
             for (int u = 0; u < kUnroll; u++) O[i + u * stride] = apply16<T, OP>(a[u], c[u]);
         }
-        for (; i < nv; i += stride) O[i] = apply16<T, OP>(X[i], Y[i]);
+        for (; i < nv; i += stride) O[i] = apply16<T, OP>(ldnt(X + i), ldnt(Y + i));
     }
 }
 
@@ -150,10 +162,10 @@ __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(uint4 *__restrict__ 
                 const uint4 *g = in + base + (size_t)u * kBlock + threadIdx.x;
                 uint4 *l = &stage[u * kBlock + wave * 64];
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
-                                                 (__attribute__((address_space(3))) void *)l, 16, 0, 0);
+                                                 (__attribute__((address_space(3))) void *)l, 16, 0, 2 /* nt */);
             }
 #pragma unroll
-            for (int u = 0; u < kUnroll; u++) a[u] = inout[base + (size_t)u * kBlock + threadIdx.x];
+            for (int u = 0; u < kUnroll; u++) a[u] = ldnt(inout + base + (size_t)u * kBlock + threadIdx.x);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
             for (int u = 0; u < kUnroll; u++)
