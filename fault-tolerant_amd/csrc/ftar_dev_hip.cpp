@@ -44,13 +44,15 @@ size_t esize_of(int dtype)
     }
 }
 
-// Streaming kernels: up to 32 workgroups of 256 threads per CU in the grid (8 resident,
-// the rest queued) -- the best grid of the C2 sweep (profiles/, tools/reduce_sweep.hip).
+// Grid cap for the streaming kernels, in 256-thread workgroups per CU.  The default
+// (1024/CU = 262144 workgroups) never binds below 2 GiB per operand: every 8 KiB tile
+// gets its own short-lived workgroup, the fastest mapping of the C2 sweep
+// (tools/reduce_sweep.hip, profiles/).
 unsigned blocks_per_cu()
 {
     const char *e = getenv("FTAR_BLOCKS_PER_CU");
-    int v = e ? atoi(e) : 32;
-    return (unsigned)(v < 1 ? 1 : v > 256 ? 256 : v);
+    int v = e ? atoi(e) : 1024;
+    return (unsigned)(v < 1 ? 1 : v > 4096 ? 4096 : v);
 }
 
 struct Pending {
@@ -308,7 +310,7 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
     bool aligned = (((uintptr_t)in | (uintptr_t)inout) & 15) == 0 && (n * es) % 16 == 0;
     if (g_reduce_variant == 1 && aligned) {
         size_t nv = n * es / 16;
-        size_t tiles = (nv + 1023) / 1024;
+        size_t tiles = (nv + ftar::kTileVecs - 1) / ftar::kTileVecs;
         unsigned grid = tiles < cached_blocks ? (unsigned)tiles : cached_blocks;
         hipError_t e = ftar::launch_reduce_lds(dtype, op, inout, in, nv, grid, s);
         if (e != hipSuccess) return set_err(e, "reduce_lds_kernel launch");

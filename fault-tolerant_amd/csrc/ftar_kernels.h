@@ -11,6 +11,7 @@ enum { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
 enum { kCopy = 0, kReduce = 1 };
 
 constexpr int kMaxKSegs = 12; // 4 user segments x (head, body, tail)
+constexpr int kTileVecs = 512; // 16-byte vectors per workgroup tile (256 threads x 2)
 
 struct KSeg {
     void *out;

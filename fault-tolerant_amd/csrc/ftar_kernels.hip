@@ -4,10 +4,10 @@
 // the operands, no reuse, no MFMA.  What matters on MI355X:
 //   * 16-byte lanes (global_load_dwordx4 / global_store_dwordx4): 1 KiB per wave
 //     instruction, the widest coalesced access;
-//   * enough bytes in flight: each lane issues UNROLL independent 16-byte non-temporal
-//     loads per operand before it consumes any (128 B per lane for a reduce); the grid
-//     has up to 32 workgroups of 4 waves per CU (8 resident = 32 waves/CU, the rest
-//     queued), the best grid of the C2 sweep;
+//   * enough bytes in flight and short-lived blocks: one 8 KiB tile per operand per
+//     256-thread workgroup, two independent 16-byte non-temporal loads per lane and
+//     operand, one tile per block (65536 workgroups for the 256 MiB C2 reduce) -- the
+//     fastest mapping of the C2 sweep (tools/reduce_sweep.hip);
 //   * one launch handles up to FDEV_MAX_KSEGS independent segments (e.g. Raben's
 //     step 0: reduce half the window + copy the other half of the partner's vector),
 //     blocks are split between segments in proportion to their bytes and each wave
@@ -65,7 +65,8 @@ __device__ __forceinline__ uint4 apply16(uint4 a, uint4 b)
 // segment kernel
 // ---------------------------------------------------------------------------------
 constexpr int kBlock = 256;
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 2;
+static_assert(kBlock * kUnroll == kTileVecs, "tile size");
 
 // Streaming operands are read once: non-temporal loads (global_load_dwordx4 ... nt) keep
 // them from displacing useful lines and measured 6.36 TB/s against 5.2-5.5 TB/s for
@@ -90,33 +91,35 @@ __device__ __forceinline__ int find_segment(const KSegList &L)
 template <typename T, int OP>
 __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk)
 {
+    // Block-contiguous tiles of kBlock * kUnroll vectors (8 KiB per operand per block):
+    // each lane issues kUnroll independent 16-byte non-temporal loads per operand, wave
+    // instructions stay 1 KiB coalesced, and the grid is sized so that one tile per block
+    // covers the segment (the loop only runs when the host capped the grid).
     constexpr size_t E = 16 / sizeof(T);
+    constexpr size_t kTile = (size_t)kBlock * kUnroll;
     const uint4 *__restrict__ X = (const uint4 *)S.x;
     const uint4 *__restrict__ Y = (const uint4 *)S.y;
     uint4 *__restrict__ O = (uint4 *)S.out;
     const size_t nv = S.n / E;
-    const size_t stride = nblk * kBlock;
-    size_t i = b * kBlock + threadIdx.x;
-    if (S.kind == kCopy) {
-        for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
-            uint4 a[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; u++) a[u] = ldnt(X + i + u * stride);
-#pragma unroll
-            for (int u = 0; u < kUnroll; u++) O[i + u * stride] = a[u];
-        }
-        for (; i < nv; i += stride) O[i] = ldnt(X + i);
-    } else {
-        for (; i + (kUnroll - 1) * stride < nv; i += kUnroll * stride) {
+    for (size_t base = b * kTile; base < nv; base += nblk * kTile) {
+        const size_t i = base + threadIdx.x;
+        if (base + kTile <= nv) {
             uint4 a[kUnroll], c[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; u++) a[u] = ldnt(X + i + u * stride);
+            for (int u = 0; u < kUnroll; u++) a[u] = ldnt(X + i + u * kBlock);
+            if (S.kind == kCopy) {
 #pragma unroll
-            for (int u = 0; u < kUnroll; u++) c[u] = ldnt(Y + i + u * stride);
+                for (int u = 0; u < kUnroll; u++) O[i + u * kBlock] = a[u];
+            } else {
 #pragma unroll
-            for (int u = 0; u < kUnroll; u++) O[i + u * stride] = apply16<T, OP>(a[u], c[u]);
+                for (int u = 0; u < kUnroll; u++) c[u] = ldnt(Y + i + u * kBlock);
+#pragma unroll
+                for (int u = 0; u < kUnroll; u++) O[i + u * kBlock] = apply16<T, OP>(a[u], c[u]);
+            }
+        } else {
+            for (size_t j = i; j < nv; j += kBlock)
+                O[j] = (S.kind == kCopy) ? ldnt(X + j) : apply16<T, OP>(ldnt(X + j), ldnt(Y + j));
         }
-        for (; i < nv; i += stride) O[i] = apply16<T, OP>(ldnt(X + i), ldnt(Y + i));
     }
 }
 
@@ -275,18 +278,19 @@ unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_bloc
         add(tail_off, g.n - tail_off, 0);
     }
     if (np == 0) return 0;
-    // blocks: scalar pieces get 1 block (they are < 16 bytes, or unaligned slow paths
-    // sized by their own length), vector pieces share the rest by bytes.
-    const size_t bytes_per_block_min = (size_t)kBlock * 16 * kUnroll; // one unrolled sweep
+    // blocks: a vector piece gets one block per tile of kBlock*kUnroll vectors (capped at
+    // max_blocks in total, pieces then loop); scalar pieces (heads/tails < 16 B, or
+    // non-co-aligned slow paths) get up to 64 blocks.
+    const size_t tile_bytes = (size_t)kBlock * 16 * kUnroll;
     unsigned next = 0;
     for (int i = 0; i < np; i++) {
         KSeg &k = pieces[i].k;
         size_t want;
         if (k.vec) {
+            size_t need = (pieces[i].bytes + tile_bytes - 1) / tile_bytes;
             size_t share = vec_bytes_total ? (size_t)((double)max_blocks * (double)pieces[i].bytes /
-                                                     (double)vec_bytes_total)
+                                                     (double)vec_bytes_total) + 1
                                            : 1;
-            size_t need = (pieces[i].bytes + bytes_per_block_min - 1) / bytes_per_block_min;
             want = need < share ? need : share;
         } else {
             size_t need = (k.n + kBlock - 1) / kBlock;

@@ -39,4 +39,13 @@ if [[ $STEPS == *pmc* ]]; then
     rc=$?; tail -2 "$OUT/pmc_$ctr.log"; stop_on_fault $rc pmc_$ctr
   done
 fi
+if [[ $STEPS == *rehearse* ]]; then
+  # multi-rank bench path with every rank on GPU 0 (gloo for the torch side)
+  for n in 2 4; do
+    FTAR_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+        --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps ${REH_STEPS:-5} \
+        --warmup 1 --dist-backend gloo > "$OUT/rehearse_$n.json" 2> "$OUT/rehearse_$n.err"
+    rc=$?; cat "$OUT/rehearse_$n.json"; tail -3 "$OUT/rehearse_$n.err"; stop_on_fault $rc rehearse_$n
+  done
+fi
 echo ALLDONE
