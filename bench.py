@@ -53,7 +53,7 @@ def pmc_traffic(name):
         return None
 
 
-def cpu_baseline_local_reduce(min_seconds=10.0, max_passes=200):
+def cpu_baseline_local_reduce(min_seconds=10.0, max_passes=2000):
     """The oracle's MPI_Reduce_local restatement on the host (1 thread), same workload."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
