@@ -117,7 +117,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->wsize = size;
     c->device = device;
     c->verbose = getenv("FTAR_VERBOSE") ? atoi(getenv("FTAR_VERBOSE")) : 0;
-    c->step_delay_s = getenv("FTAR_STEP_DELAY_MS") ? atof(getenv("FTAR_STEP_DELAY_MS")) * 1e-3 : 0.0;
+    c->loop_seconds = getenv("FTAR_LOOP_SECONDS") ? atof(getenv("FTAR_LOOP_SECONDS")) : 0.0;
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
     if (rc) {
@@ -258,12 +258,17 @@ int ftar_barrier(ftar_comm *c)
 
 /* ---- synchronisation ------------------------------------------------------ */
 
+uint64_t ftar_step_sync(ftar_comm *c, int nsteps)
+{
+    if (c->loop_seconds > 0 && nsteps > 0) { /* busy (R state), like a rank inside its exchange */
+        double t0 = now_s(), d = c->loop_seconds / nsteps;
+        while (now_s() - t0 < d) ftar_ctrl_poll(&c->job);
+    }
+    return ftar_sync(c);
+}
+
 uint64_t ftar_sync(ftar_comm *c)
 {
-    if (c->step_delay_s > 0) { /* busy (R state), like a rank still inside its exchange */
-        double t0 = now_s();
-        while (now_s() - t0 < c->step_delay_s) ftar_ctrl_poll(&c->job);
-    }
     uint64_t next = c->job.seq + 1;
     atomic_store_explicit(&c->job.shm->slot[c->wrank].pubv[next % 2], (next << 16) | ((uint64_t)c->pubval & 0xffff),
                           memory_order_release);

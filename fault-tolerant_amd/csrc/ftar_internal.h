@@ -48,7 +48,7 @@ struct ftar_comm {
     int profiling;
     ftar_stats stats;
     int verbose;
-    double step_delay_s; /* FTAR_STEP_DELAY_MS: stretch every tolerant barrier (harness knob) */
+    double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
 };
 
 size_t ftar_esize(int dtype);
@@ -62,6 +62,9 @@ void *ftar_buf(ftar_comm *c, int w, int b);
 
 /* agree over the survivors; returns newly failed original ranks (not yet acked) */
 uint64_t ftar_sync(ftar_comm *c);
+/* the per-step agree of a schedule loop; `nsteps` = steps of the loop (spreads the
+ * FTAR_LOOP_SECONDS harness delay over them) */
+uint64_t ftar_step_sync(ftar_comm *c, int nsteps);
 /* value original rank w published before the last completed sync */
 int64_t ftar_peer_pub(ftar_comm *c, int w);
 /* agree outside the tolerant region: any new failure aborts the job */

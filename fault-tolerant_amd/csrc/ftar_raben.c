@@ -288,7 +288,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_AFTER);
         }
         ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BARRIER);
-        uint64_t newf = ftar_sync(c); /* agree + barrier (:258-265) */
+        uint64_t newf = ftar_step_sync(c, 2 * x->steps); /* agree + barrier (:258-265) */
         if (newf) rb_handler_rs(x, newf, step);
     }
 
@@ -308,7 +308,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         }
         ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_AFTER);
         ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BARRIER);
-        uint64_t newf = ftar_sync(c);
+        uint64_t newf = ftar_step_sync(c, 2 * x->steps); /* (:330-335) */
         if (newf) rb_handler_ag(x, newf, step);
     }
 

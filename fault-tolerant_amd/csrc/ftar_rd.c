@@ -236,7 +236,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
         }
         ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_AFTER);
         ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BARRIER);
-        newf = ftar_sync(c); /* agree + barrier (:51-53) */
+        newf = ftar_step_sync(c, ftar_hibit(x->nactive, 31) > 0 ? ftar_hibit(x->nactive, 31) : 1); /* (:51-53) */
         if (newf) {
             int dd = rd_handler(x, newf, distance * 2);
             distance = dd / 2;
