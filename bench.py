@@ -108,8 +108,40 @@ def single(args):
                      "kernel": "segment_kernel<float,SUM>", "algorithmic_bytes_per_launch": 3 * S,
                      "kernel_ms": round(k_ms, 4)},
     }
+    out["e2e"] = e2e_local(ftar, args.count)
     out["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_local_reduce()
     print(json.dumps(out), flush=True)
+
+
+def e2e_local(ftar, count, iters=5):
+    """Host-resident variant of the same step: pinned H2D of both vectors, the kernel,
+    pinned D2H of the result (PCIe-bound), never the headline value."""
+    import torch
+    xh = torch.rand(count).pin_memory()
+    yh = torch.rand(count).pin_memory()
+    xd = torch.empty(count, device="cuda")
+    yd = torch.empty(count, device="cuda")
+    S = count * 4
+    ts = {"h2d": 0.0, "d2h": 0.0, "total": 0.0}
+    for _ in range(iters):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        xd.copy_(xh, non_blocking=True)
+        yd.copy_(yh, non_blocking=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ftar.reduce_local(xd, yd)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        yh.copy_(yd, non_blocking=True)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        ts["h2d"] += t1 - t0
+        ts["d2h"] += t3 - t2
+        ts["total"] += t3 - t0
+    return {"h2d_GBps": round(2 * S * iters / ts["h2d"] / 1e9, 2), "d2h_GBps": round(S * iters / ts["d2h"] / 1e9, 2),
+            "ms": round(ts["total"] * 1e3 / iters, 3),
+            "GBps": round(2 * S * iters / ts["total"] / 1e9, 2)}
 
 
 def multi(args):
@@ -167,6 +199,18 @@ def multi(args):
     raben()
     err = (y.cpu() - ref.cpu()).abs().max().item()
     t_rd, k_rd = timed(rd)
+    # end-to-end with host buffers: pinned H2D + device Allreduce + D2H (never the value)
+    xh = x.cpu().pin_memory()
+    yh = torch.empty_like(xh).pin_memory()
+
+    def raben_host():
+        rc = comm.allreduce_rabenseifner_host(xh, yh)
+        assert rc == 0, rc
+
+    saved = (args.steps, args.warmup)
+    args.steps, args.warmup = 3, 1
+    t_e2e, _ = timed(raben_host)
+    args.steps, args.warmup = saved
     t_nc = None
     if args.dist_backend == "nccl":
         z = x.clone()
@@ -198,6 +242,7 @@ def multi(args):
                          "frac": round(achieved / XGMI_LINK_GBS, 4) if achieved else None, "traffic": None,
                          "kernel": "Raben RS step 0 (pull full partner vector, reduce half)",
                          "algorithmic_bytes_per_launch": S, "kernel_ms": round(k_rb, 4)},
+            "e2e_host_buffers": {"ms_per_step": round(t_e2e * 1e3, 3), "algbw_GBps": round(S / t_e2e / 1e9, 2)},
             "rd": {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
                    "step0_kernel_ms": round(k_rd, 4)},
             "rccl_allreduce": ({"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2)}

@@ -199,6 +199,14 @@ class Comm:
             dtype = _dtype_of(rbuf)
         return lib().ftar_allreduce_rabenseifner(_ptr(sbuf), _ptr(rbuf), count, dtype, op, self._h)
 
+    def allreduce_rabenseifner_host(self, sbuf, rbuf, count=None, dtype=None, op: int = SUM) -> int:
+        """Host buffers (ideally pinned torch CPU tensors): H2D, device Allreduce, D2H."""
+        if count is None:
+            count = rbuf.numel()
+        if dtype is None:
+            dtype = _dtype_of(rbuf)
+        return lib().ftar_allreduce_rabenseifner_host(sbuf.data_ptr(), rbuf.data_ptr(), count, dtype, op, self._h)
+
     def recursive_doubling(self, src, dst, count=None, dtype=None, op: int = SUM) -> int:
         if count is None:
             count = dst.numel()

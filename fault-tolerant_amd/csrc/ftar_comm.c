@@ -69,15 +69,19 @@ static void recompute_members(ftar_comm *c)
 
 /* ---- fault injection ---------------------------------------------------- */
 
-static int parse_kills(const char *s, ftar_kill *out, int max)
+/* "rank:phase:step:point[:call]" entries separated by ',' (call = 0-based index of the
+ * allreduce call on that rank; omitted = every call) */
+static int parse_kills(const char *s, ftar_kill *out, int *call, int max)
 {
     int n = 0;
     while (s && *s && n < max) {
         ftar_kill k;
-        int used = 0;
+        int used = 0, cl = -1, used2 = 0;
         if (sscanf(s, "%d:%d:%d:%d%n", &k.rank, &k.phase, &k.step, &k.point, &used) != 4) break;
-        out[n++] = k;
         s += used;
+        if (*s == ':' && sscanf(s, ":%d%n", &cl, &used2) == 1) s += used2;
+        call[n] = cl;
+        out[n++] = k;
         while (*s == ',' || *s == ' ' || *s == ';') s++;
     }
     return n;
@@ -88,6 +92,7 @@ void ftar_maybe_die(ftar_comm *c, int phase, int step, int point)
     for (int i = 0; i < c->nkills; i++) {
         const ftar_kill *k = &c->kills[i];
         if (k->rank != c->wrank || k->phase != phase || k->step != step || k->point != point) continue;
+        if (c->kill_call[i] >= 0 && c->kill_call[i] != c->ncalls - 1) continue;
         if (point == FTAR_PT_BARRIER) /* let every peer finish the step first */
             ftar_ctrl_wait_peers_arrived(&c->job, c->members, c->job.seq + 1);
         if (c->verbose) fprintf(stderr, "ftar: rank %d dies at phase %d step %d point %d\n", c->wrank, phase, step, point);
@@ -101,6 +106,7 @@ int ftar_set_kills(ftar_comm *c, const ftar_kill *kills, int nkills)
 {
     if (!c || nkills < 0 || nkills > FTAR_MAX_KILLS) return FTAR_ERR_ARG;
     memcpy(c->kills, kills, sizeof(ftar_kill) * (size_t)nkills);
+    for (int i = 0; i < nkills; i++) c->kill_call[i] = -1;
     c->nkills = nkills;
     return FTAR_SUCCESS;
 }
@@ -143,7 +149,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     recompute_members(c);
     c->acked = 0;
     const char *ks = getenv("FTAR_KILL");
-    if (ks) c->nkills = parse_kills(ks, c->kills, FTAR_MAX_KILLS);
+    if (ks) c->nkills = parse_kills(ks, c->kills, c->kill_call, FTAR_MAX_KILLS);
     /* every rank has mapped the control block once this round completes */
     ftar_sync_fatal(c);
     if (rank == 0) shm_unlink(job);
@@ -392,6 +398,7 @@ static double g_t0;
 
 void ftar_stats_begin(ftar_comm *c)
 {
+    c->ncalls++;
     memset(&c->stats, 0, sizeof(c->stats));
     fdev_counters_reset(c->dev);
     g_t0 = now_s();

@@ -31,7 +31,9 @@ struct ftar_comm {
     uint64_t acked;   /* failures already acknowledged (MPIX_Comm_failure_ack) */
 
     ftar_kill kills[FTAR_MAX_KILLS];
+    int kill_call[FTAR_MAX_KILLS]; /* call index the kill applies to, -1 = every call */
     int nkills;
+    int ncalls; /* allreduce calls started on this rank */
 
     /* exported workspace and the peers' mappings of theirs */
     void *ws[FTAR_NBUF];

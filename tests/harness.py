@@ -26,7 +26,7 @@ class ProbeRun:
     stdout: str
     stderr: str
     outputs: dict      # rank -> list of np arrays (one per iteration)
-    status: dict       # rank -> list of (rc, comm_rank, comm_size, recoveries)
+    status: dict       # rank -> list of (rc, comm_rank, comm_size, recoveries, wall_us)
 
     @property
     def aborted(self) -> bool:
@@ -34,7 +34,8 @@ class ProbeRun:
 
 
 def kill_env(kills) -> str:
-    return ",".join(f"{r}:{ph}:{st}:{pt}" for (r, ph, st, pt) in kills)
+    """(rank, phase, step, point[, call]) tuples -> FTAR_KILL."""
+    return ",".join(":".join(str(v) for v in k) for k in kills)
 
 
 def run_probe(algo: str, inputs, kills=(), op: int = 0, iters: int = 1, backend: str = "hostsim",

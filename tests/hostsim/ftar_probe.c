@@ -56,7 +56,7 @@ int main(void)
         fclose(f);
         snprintf(path, sizeof(path), "%s/status_%d_%d.txt", dir, rank, it);
         f = fopen(path, "w");
-        fprintf(f, "%d %d %d %d\n", rc, crank, csize, st.recoveries);
+        fprintf(f, "%d %d %d %d %lld\n", rc, crank, csize, st.recoveries, (long long)(st.wall_s * 1e6));
         fclose(f);
     }
     ftar_finalize(comm);

@@ -92,7 +92,7 @@ def test_repeated_calls_and_retargeted_comm(hostsim, oracle):
     o2 = oracle.rabenseifner([inputs[w] for w in order])
     for i, w in enumerate(order):
         assert np.array_equal(r.outputs[w][0].view(np.uint32), o1.outputs[w].view(np.uint32))
-        assert r.status[w][0][1:] == (i, 4, 1)      # comm rank, size, recoveries after the call
+        assert r.status[w][0][1:4] == (i, 4, 1)      # comm rank, size, recoveries after the call
         for it in (1, 2):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o2.outputs[i].view(np.uint32))
 
