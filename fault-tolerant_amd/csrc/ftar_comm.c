@@ -275,10 +275,16 @@ uint64_t ftar_step_sync(ftar_comm *c, int nsteps)
 
 uint64_t ftar_sync(ftar_comm *c)
 {
+    double t0 = now_s();
     uint64_t next = c->job.seq + 1;
     atomic_store_explicit(&c->job.shm->slot[c->wrank].pubv[next % 2], (next << 16) | ((uint64_t)c->pubval & 0xffff),
                           memory_order_release);
     uint64_t snap = ftar_ctrl_agree(&c->job, c->members);
+    double dt = now_s() - t0;
+    c->stats.sync_wait_s += dt;
+    c->stats.syncs++;
+    if (c->verbose >= 2)
+        fprintf(stderr, "ftar[%d] sync %llu waited %.3f ms\n", c->wrank, (unsigned long long)c->job.seq, dt * 1e3);
     return snap & ~c->acked;
 }
 
@@ -307,7 +313,9 @@ int ftar_is_dead(ftar_comm *c, int w) { return ftar_ctrl_is_dead(&c->job, w); }
 
 int ftar_drain(ftar_comm *c)
 {
+    double t0 = now_s();
     int rc = fdev_sync(c->dev, ftar_ctrl_poll, &c->job);
+    c->stats.drain_s += now_s() - t0;
     if (rc) {
         fprintf(stderr, "ftar: rank %d: device error: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);

@@ -164,6 +164,9 @@ typedef struct {
     double link_bytes;       /* bytes this rank pulled over the fabric (algorithmic) */
     double hbm_bytes;        /* algorithmic HBM bytes of this rank's kernels */
     int    kernels;          /* kernels launched */
+    double sync_wait_s;      /* host time spent in agree/barrier rounds */
+    double drain_s;          /* host time spent waiting for the device stream */
+    int    syncs;            /* agree/barrier rounds */
 } ftar_stats;
 
 int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);

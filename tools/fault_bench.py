@@ -31,8 +31,10 @@ def run(count, kill):
         if o.status[w] == 0 and ok:
             ok &= np.array_equal(r.outputs[w][1].view(np.uint32), o.outputs[w].view(np.uint32))
     walls = [st[4] / 1e3 for st in r.status.get(0, [])]
+    per_rank = {w: [{"wall_ms": s[4] / 1e3, "sync_ms": s[5] / 1e3, "drain_ms": s[6] / 1e3, "syncs": s[7]}
+                    for s in r.status[w]] for w in r.status}
     return {"kill": kill, "aborted": r.aborted, "parity_ok": bool(ok), "rank0_call_ms": walls,
-            "recoveries": [st[3] for st in r.status.get(0, [])]}
+            "recoveries": [st[3] for st in r.status.get(0, [])], "per_rank": per_rank}
 
 
 def main():
