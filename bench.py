@@ -181,6 +181,7 @@ def multi(args):
         if args.dist_backend == "nccl":
             t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        timed.link_bytes = comm.last_stats().step0_link_bytes
         return t[0].item() / args.steps, t[1].item() / args.steps
 
     def raben():
@@ -192,6 +193,7 @@ def multi(args):
         assert rc == 0, rc
 
     t_rb, k_rb = timed(raben)
+    step0_bytes = timed.link_bytes
     # correctness spot check against torch.distributed's all_reduce on the same inputs
     # (fp32, different reduction order: |err| <= log2(p) * 2^-24 * sum|x_i|)
     ref = x.clone() if args.dist_backend == "nccl" else x.cpu()
@@ -221,9 +223,13 @@ def multi(args):
         t_nc, _ = timed(rccl)
     L = world.bit_length() - 1
     pow2 = (1 << L) == world
-    link_bytes_raben = (2.5 - 2.0 ** (1 - L)) * S if pow2 else None
+    # link bytes per rank per direction on the critical path (SURVEY.md 8d counts the
+    # step-0 full exchange, (2.5 - 2^(1-L)) S; with the redundancy half overlapped on the
+    # background stream the critical path carries 2 (1 - 2^-L) S, classic Rabenseifner)
+    link_bytes_raben = ((2.5 - 2.0 ** (1 - L)) * S if os.environ.get("FTAR_OVERLAP", "1") == "0"
+                        else 2 * (1 - 2.0 ** -L) * S) if pow2 else None
     t_roof = link_bytes_raben / (XGMI_LINK_GBS * 1e9) if link_bytes_raben else None
-    achieved = S / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None         # RS step-0 kernel pulls S bytes
+    achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernel's pulled bytes
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(world * S / t_rb / 1e9, 2), "unit": "GB/s", "n_gpus": world,
@@ -240,8 +246,8 @@ def multi(args):
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
                          "peak": XGMI_LINK_GBS, "unit": "GB/s",
                          "frac": round(achieved / XGMI_LINK_GBS, 4) if achieved else None, "traffic": None,
-                         "kernel": "Raben RS step 0 (pull full partner vector, reduce half)",
-                         "algorithmic_bytes_per_launch": S, "kernel_ms": round(k_rb, 4)},
+                         "kernel": "Raben RS step 0 reduce half (pull partner's half, reduce into W)",
+                         "algorithmic_bytes_per_launch": step0_bytes, "kernel_ms": round(k_rb, 4)},
             "e2e_host_buffers": {"ms_per_step": round(t_e2e * 1e3, 3), "algbw_GBps": round(S / t_e2e / 1e9, 2)},
             "rd": {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
                    "step0_kernel_ms": round(k_rd, 4)},

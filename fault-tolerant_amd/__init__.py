@@ -35,7 +35,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("steps", ctypes.c_int), ("recoveries", ctypes.c_int), ("comm_size_after", ctypes.c_int),
                 ("wall_s", ctypes.c_double), ("kernel_ms", ctypes.c_double),
                 ("step0_kernel_ms", ctypes.c_double), ("link_bytes", ctypes.c_double),
-                ("hbm_bytes", ctypes.c_double), ("kernels", ctypes.c_int), ("sync_wait_s", ctypes.c_double),
+                ("hbm_bytes", ctypes.c_double), ("kernels", ctypes.c_int), ("step0_link_bytes", ctypes.c_double),
+                ("bg_kernel_ms", ctypes.c_double), ("sync_wait_s", ctypes.c_double),
                 ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int)]
 
 

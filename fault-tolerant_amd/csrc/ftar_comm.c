@@ -124,6 +124,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->device = device;
     c->verbose = getenv("FTAR_VERBOSE") ? atoi(getenv("FTAR_VERBOSE")) : 0;
     c->loop_seconds = getenv("FTAR_LOOP_SECONDS") ? atof(getenv("FTAR_LOOP_SECONDS")) : 0.0;
+    c->overlap = getenv("FTAR_OVERLAP") ? atoi(getenv("FTAR_OVERLAP")) : 1;
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
     if (rc) {
@@ -323,6 +324,28 @@ int ftar_drain(ftar_comm *c)
     return rc;
 }
 
+int ftar_drain_bg(ftar_comm *c)
+{
+    double t0 = now_s();
+    int rc = fdev_sync_bg(c->dev, ftar_ctrl_poll, &c->job);
+    c->stats.drain_s += now_s() - t0;
+    if (rc) {
+        fprintf(stderr, "ftar: rank %d: device error: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    return rc;
+}
+
+int ftar_run_bg(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    int rc = fdev_run_bg(c->dev, dtype, op, segs, nseg, tag);
+    if (rc) {
+        fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    return rc;
+}
+
 int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     int rc = fdev_run(c->dev, dtype, op, segs, nseg, tag);
@@ -417,11 +440,12 @@ void ftar_stats_end(ftar_comm *c)
     fdev_counters k;
     fdev_counters_get(c->dev, &k);
     c->stats.wall_s = now_s() - g_t0;
-    c->stats.kernel_ms = k.ms[0] + k.ms[1] + k.ms[2] + k.ms[3];
+    c->stats.kernel_ms = k.ms[0] + k.ms[1] + k.ms[2] + k.ms[3] + k.ms[4];
+    c->stats.bg_kernel_ms = k.ms[FDEV_TAG_BG];
     c->stats.step0_kernel_ms = k.ms[FDEV_TAG_STEP0];
     c->stats.link_bytes = k.link_bytes;
     c->stats.hbm_bytes = k.hbm_bytes;
-    c->stats.kernels = k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3];
+    c->stats.kernels = k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3] + k.launches[4];
     c->stats.comm_size_after = c->size;
 }
 

@@ -46,7 +46,8 @@ typedef struct {
 #define FDEV_TAG_STEP0 1   /* dominant exchange kernel: Raben RS step 0 / RD step */
 #define FDEV_TAG_STEP 2    /* other exchange kernels */
 #define FDEV_TAG_RECOV 3   /* recovery transfers */
-#define FDEV_NTAGS 4
+#define FDEV_TAG_BG 4      /* background stream (Raben step-0 redundancy copy) */
+#define FDEV_NTAGS 5
 
 typedef struct ftar_dev ftar_dev;
 
@@ -69,6 +70,11 @@ int fdev_unimport(ftar_dev *d, void *ptr);
 
 /* Enqueue one segment kernel on the rank's stream. */
 int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+/* Enqueue on the rank's background stream, ordered after everything queued so far on
+ * the main stream (it then overlaps later main-stream work). */
+int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+/* Spin until the background stream drained. */
+int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg);
 /* Make the rank's stream wait for everything queued on `user_stream` (hipStream_t). */
 int fdev_order_after(ftar_dev *d, void *user_stream);
 /* Spin (busy, the process stays in R state) until the stream drained.  `poll` is

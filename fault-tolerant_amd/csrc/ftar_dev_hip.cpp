@@ -65,6 +65,7 @@ struct Pending {
 struct ftar_dev {
     int device;
     hipStream_t stream;
+    hipStream_t bg;
     int profiling;
     unsigned max_blocks;
     std::vector<Pending> pending;
@@ -101,6 +102,7 @@ int fdev_open(int device, ftar_dev **out)
     d->max_blocks = (unsigned)prop.multiProcessorCount * blocks_per_cu();
     if (d->max_blocks == 0) d->max_blocks = 2048;
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&d->bg, hipStreamNonBlocking));
     // Peer access to every other GPU of the node: the exchanges read peers' HBM.
     for (int p = 0; p < ndev; p++) {
         if (p == device) continue;
@@ -119,12 +121,14 @@ void fdev_close(ftar_dev *d)
     if (!d) return;
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->stream);
+    (void)hipStreamSynchronize(d->bg);
     for (auto &p : d->pending) {
         (void)hipEventDestroy(p.start);
         (void)hipEventDestroy(p.stop);
     }
     for (auto e : d->event_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
+    (void)hipStreamDestroy(d->bg);
     delete d;
 }
 
@@ -190,7 +194,7 @@ static hipEvent_t get_event(ftar_dev *d)
     return e;
 }
 
-int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     size_t es = esize_of(dtype);
     if (es == 0 || op < 0 || op > 3 || nseg < 0 || nseg > FDEV_MAX_SEGS || tag < 0 || tag >= FDEV_NTAGS) {
@@ -218,15 +222,30 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
     if (d->profiling) {
         e0 = get_event(d);
         e1 = get_event(d);
-        if (e0) (void)hipEventRecord(e0, d->stream);
+        if (e0) (void)hipEventRecord(e0, st);
     }
-    hipError_t e = ftar::launch_segments(dtype, op, L, grid, d->stream);
+    hipError_t e = ftar::launch_segments(dtype, op, L, grid, st);
     if (e != hipSuccess) return set_err(e, "segment_kernel launch");
     if (d->profiling && e0 && e1) {
-        (void)hipEventRecord(e1, d->stream);
+        (void)hipEventRecord(e1, st);
         d->pending.push_back(Pending{e0, e1, tag});
     }
     return 0;
+}
+
+int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    return run_on(d, d->stream, dtype, op, segs, nseg, tag);
+}
+
+int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    hipEvent_t e = get_event(d);
+    if (!e) return set_err(hipErrorOutOfMemory, "hipEventCreate");
+    HIPCHK(hipEventRecord(e, d->stream));
+    HIPCHK(hipStreamWaitEvent(d->bg, e, 0));
+    d->event_pool.push_back(e);
+    return run_on(d, d->bg, dtype, op, segs, nseg, tag);
 }
 
 int fdev_order_after(ftar_dev *d, void *user_stream)
@@ -239,10 +258,12 @@ int fdev_order_after(ftar_dev *d, void *user_stream)
     return 0;
 }
 
-int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
+static int harvest(ftar_dev *d);
+
+static int sync_stream(ftar_dev *d, hipStream_t st, int (*poll)(void *), void *arg)
 {
     for (;;) {
-        hipError_t e = hipStreamQuery(d->stream);
+        hipError_t e = hipStreamQuery(st);
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) return set_err(e, "hipStreamQuery");
         if (poll) {
@@ -250,7 +271,32 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
             if (r) return r;
         }
     }
+    return 0;
+}
+
+int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
+{
+    int rc = sync_stream(d, d->stream, poll, arg);
+    if (rc) return rc;
+    return harvest(d);
+}
+
+int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg)
+{
+    int rc = sync_stream(d, d->bg, poll, arg);
+    if (rc) return rc;
+    return harvest(d);
+}
+
+/* collect the timings of every event pair whose stop event has completed */
+static int harvest(ftar_dev *d)
+{
+    std::vector<Pending> still;
     for (auto &p : d->pending) {
+        if (hipEventQuery(p.stop) != hipSuccess) {
+            still.push_back(p);
+            continue;
+        }
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess) {
             d->ctr.ms[p.tag] += ms;
@@ -259,7 +305,7 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
         d->event_pool.push_back(p.start);
         d->event_pool.push_back(p.stop);
     }
-    d->pending.clear();
+    d->pending.swap(still);
     return 0;
 }
 

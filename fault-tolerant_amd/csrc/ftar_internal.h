@@ -50,6 +50,7 @@ struct ftar_comm {
     int profiling;
     ftar_stats stats;
     int verbose;
+    int overlap;         /* FTAR_OVERLAP (default 1): Raben step-0 redundancy copy on the background stream */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
 };
 
@@ -75,6 +76,9 @@ void ftar_sync_fatal(ftar_comm *c);
 int ftar_drain(ftar_comm *c);
 /* enqueue one segment kernel */
 int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+/* enqueue on the background stream (after the main stream's current work) */
+int ftar_run_bg(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+int ftar_drain_bg(ftar_comm *c);
 int ftar_is_dead(ftar_comm *c, int w);
 
 /* deterministic fault injection at (phase, step, point) */

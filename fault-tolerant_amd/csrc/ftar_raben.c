@@ -38,6 +38,7 @@ typedef struct {
     size_t es, count;
     int steps, adjsize, rem;
     int rank, vrank, corr, has_recov;
+    int bg_pending; /* step-0 redundancy copy still running on the background stream */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
 } rb_ctx;
 
@@ -113,6 +114,10 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
         rb_windows(vdead, x->count, x->steps, dri, dsi, drc, dsc);
         if (x->rank == org) {
             if (!x->has_recov) ftar_abort(c, 1); /* deviation: no step-0 copy to replay from */
+            if (x->bg_pending) { /* the dead rank's half of its vector must be in T */
+                ftar_drain_bg(c);
+                x->bg_pending = 0;
+            }
             /* replay the dead rank's steps 0..fs (:106-200) into W's half this rank sent at
              * step 0 (= the dead rank's reduce window, unused here until the allgather) */
             void *W = c->ws[WS_W], *IN = c->ws[WS_IN], *T = c->ws[WS_T];
@@ -266,6 +271,11 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             if (ftar_is_dead(c, pw)) {
                 x->corr = 1; /* the exchange failed (:238-241) */
             } else if (step == 0) {
+                /* :206-211 full exchange + :231-237 reduce.  The reduce half is on the
+                 * critical path; the redundancy half (kept in T for recovery, :191-197) is
+                 * only needed by a later error handler, so it runs on the background stream
+                 * and overlaps steps 1.. (joined before any replay and before the final
+                 * barrier).  FTAR_OVERLAP=0 keeps both halves in one launch. */
                 void *PIN = ftar_buf(c, pw, WS_IN);
                 fdev_seg s[2] = {
                     {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, x->rindex[0]), at(x, IN, x->rindex[0]),
@@ -273,7 +283,15 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                     {FDEV_COPY, FDEV_REMOTE_X, at(x, T, x->sindex[0]), at(x, PIN, x->sindex[0]), NULL,
                      (size_t)x->scount[0]},
                 };
-                ftar_run(c, x->dtype, x->op, s, 2, FDEV_TAG_STEP0);
+                if (c->overlap) {
+                    ftar_run(c, x->dtype, x->op, &s[0], 1, FDEV_TAG_STEP0);
+                    ftar_run_bg(c, x->dtype, x->op, &s[1], 1, FDEV_TAG_BG);
+                    x->bg_pending = 1;
+                    c->stats.step0_link_bytes = (double)x->rcount[0] * (double)x->es;
+                } else {
+                    ftar_run(c, x->dtype, x->op, s, 2, FDEV_TAG_STEP0);
+                    c->stats.step0_link_bytes = (double)count * (double)x->es;
+                }
                 ftar_drain(c);
             } else {
                 void *PW = ftar_buf(c, pw, WS_W);
@@ -310,6 +328,11 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BARRIER);
         uint64_t newf = ftar_step_sync(c, 2 * x->steps); /* (:330-335) */
         if (newf) rb_handler_ag(x, newf, step);
+    }
+
+    if (x->bg_pending) { /* peers read our IN until their copies are done: join before the barrier */
+        ftar_drain_bg(c);
+        x->bg_pending = 0;
     }
 
     /* ---- ERRORS_ARE_FATAL barrier + post-step (:357-381) ---- */

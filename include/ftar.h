@@ -164,6 +164,8 @@ typedef struct {
     double link_bytes;       /* bytes this rank pulled over the fabric (algorithmic) */
     double hbm_bytes;        /* algorithmic HBM bytes of this rank's kernels */
     int    kernels;          /* kernels launched */
+    double step0_link_bytes; /* fabric bytes the dominant kernel pulls per call */
+    double bg_kernel_ms;     /* device time of background-stream kernels (Raben redundancy copy) */
     double sync_wait_s;      /* host time spent in agree/barrier rounds */
     double drain_s;          /* host time spent waiting for the device stream */
     int    syncs;            /* agree/barrier rounds */

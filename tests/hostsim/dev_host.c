@@ -173,6 +173,13 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
     return 0;
 }
 
+int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    return fdev_run(d, dtype, op, segs, nseg, tag);
+}
+
+int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg) { return poll ? poll(arg) : 0; }
+
 int fdev_order_after(ftar_dev *d, void *s) { return 0; }
 
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
