@@ -37,7 +37,7 @@ class Stats(ctypes.Structure):
                 ("step0_kernel_ms", ctypes.c_double), ("link_bytes", ctypes.c_double),
                 ("hbm_bytes", ctypes.c_double), ("kernels", ctypes.c_int), ("step0_link_bytes", ctypes.c_double),
                 ("bg_kernel_ms", ctypes.c_double), ("sync_wait_s", ctypes.c_double),
-                ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int)]
+                ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int), ("relayed_steps", ctypes.c_int)]
 
 
 class Kill(ctypes.Structure):

@@ -125,6 +125,8 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->verbose = getenv("FTAR_VERBOSE") ? atoi(getenv("FTAR_VERBOSE")) : 0;
     c->loop_seconds = getenv("FTAR_LOOP_SECONDS") ? atof(getenv("FTAR_LOOP_SECONDS")) : 0.0;
     c->overlap = getenv("FTAR_OVERLAP") ? atoi(getenv("FTAR_OVERLAP")) : 1;
+    c->relay = getenv("FTAR_RELAY") ? atoi(getenv("FTAR_RELAY")) : 1;
+    c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)1 << 20);
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
     if (rc) {
@@ -447,6 +449,13 @@ void ftar_stats_end(ftar_comm *c)
     c->stats.hbm_bytes = k.hbm_bytes;
     c->stats.kernels = k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3] + k.launches[4];
     c->stats.comm_size_after = c->size;
+}
+
+double ftar_link_bytes(ftar_comm *c)
+{
+    fdev_counters k;
+    fdev_counters_get(c->dev, &k);
+    return k.link_bytes;
 }
 
 int ftar_last_stats(const ftar_comm *c, ftar_stats *out)

@@ -94,7 +94,14 @@ int ftar_ctrl_attach(ftar_job *job, const char *name, int rank, int size, int cr
         int fd = shm_open(name, O_RDWR, 0600);
         if (fd >= 0) {
             struct stat st;
-            if (fstat(fd, &st) == 0 && (size_t)st.st_size >= sizeof(ftar_shm)) {
+            if (fstat(fd, &st) == 0 && st.st_size > 0 && (size_t)st.st_size != sizeof(ftar_shm)) {
+                fprintf(stderr, "ftar: rank %d: control block %s has %lld bytes, this build expects %zu "
+                                "(launcher and library from different builds?)\n",
+                        rank, name, (long long)st.st_size, sizeof(ftar_shm));
+                close(fd);
+                return FTAR_ERR_STATE;
+            }
+            if (fstat(fd, &st) == 0 && (size_t)st.st_size == sizeof(ftar_shm)) {
                 int rc = map_segment(job, fd);
                 close(fd);
                 if (rc) return rc;

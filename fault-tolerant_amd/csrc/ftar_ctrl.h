@@ -26,7 +26,7 @@
 
 #define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
 #define FTAR_SHM_VERSION 1
-#define FTAR_NBUF 3       /* exported workspace buffers per rank */
+#define FTAR_NBUF 4       /* exported workspace buffers per rank (IN, W, T, R) */
 #define FTAR_DECISIONS 64 /* ring of agree decisions */
 
 #define FTAR_SLOT_EMPTY 0

@@ -39,7 +39,7 @@ typedef struct {
     size_t n;         /* elements */
 } fdev_seg;
 
-#define FDEV_MAX_SEGS 4
+#define FDEV_MAX_SEGS 16 /* a relayed exchange step: 2 own pulls + 2 x 6 relay duties */
 
 /* kernel tags (profiling buckets) */
 #define FDEV_TAG_LOCAL 0   /* local copies */

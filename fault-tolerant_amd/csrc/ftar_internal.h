@@ -15,6 +15,7 @@
 #define WS_IN 0  /* this rank's input vector (Raben: after the pre-step) */
 #define WS_W 1   /* accumulator: Raben rbuf, RD ping-pong A */
 #define WS_T 2   /* Raben tmp (step-0 redundancy copy), RD ping-pong B */
+#define WS_R 3   /* relay staging: stripes this rank forwards for other ranks */
 
 
 struct ftar_comm {
@@ -51,6 +52,8 @@ struct ftar_comm {
     ftar_stats stats;
     int verbose;
     int overlap;         /* FTAR_OVERLAP (default 1): Raben step-0 redundancy copy on the background stream */
+    int relay;           /* FTAR_RELAY (default 1): stripe exchanges over 2-hop paths */
+    size_t relay_min;    /* FTAR_RELAY_MIN bytes: smallest per-rank window that is relayed */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
 };
 
@@ -91,6 +94,42 @@ void ftar_shrink(ftar_comm *c, uint64_t failed);
 
 void ftar_stats_begin(ftar_comm *c);
 void ftar_stats_end(ftar_comm *c);
+
+/* ---- exchange transport (ftar_xfer.c) ------------------------------------
+ * One exchange step of a schedule, described for EVERY receiving rank so each rank
+ * can work out its relay duties.  A pull moves a window [off, off+n) of buffer src_buf
+ * of original rank `src` into buffer dst_buf of the receiver (COPY), or reduces it
+ * with the receiver's x_buf window (REDUCE; `swap` puts the pulled operand first). */
+typedef struct {
+    int kind, swap;
+    int src, src_buf;
+    int dst_buf, x_buf;
+    int64_t off, n;
+} ftar_pull;
+
+#define FTAR_MAX_PULLS 2
+typedef struct {
+    int npull[FTAR_MAX_RANKS];                   /* by comm rank; 0 = not receiving */
+    ftar_pull pull[FTAR_MAX_RANKS][FTAR_MAX_PULLS];
+} ftar_plan;
+
+typedef struct {
+    int relayed;       /* the step used 2-hop relays */
+    int skipped;       /* this rank did not pull (its source was dead at the start) */
+    uint64_t mid_dead; /* failures seen at the mid-step barrier (uniform) */
+    int missing;       /* this rank lost stripes of relays that died before the barrier */
+} ftar_xstate;
+
+void ftar_plan_clear(ftar_plan *p);
+/* phase 1 (+ mid barrier + phase 2 when relayed); `skip` = this rank's source is dead;
+ * (kphase, kstep) place the FTAR_PT_AFTER injection point after phase 1 */
+void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag, int skip, int kphase, int kstep,
+                    ftar_xstate *st);
+/* after the step's agree returned `known`: re-pull stripes lost with relays that died
+ * before the mid barrier, then one more (uniform) barrier */
+void ftar_xfer_repair(ftar_comm *c, const ftar_plan *p, int dtype, int op, ftar_xstate *st, uint64_t known);
+double ftar_link_bytes(ftar_comm *c);
+int ftar_xfer_would_relay(ftar_comm *c, const ftar_plan *p, size_t es);
 
 int ftar_hibit(int value, int start);
 int ftar_floor_pow2(int n);

@@ -10,7 +10,7 @@ enum { kInt32 = 0, kFloat32 = 1, kInt64 = 2, kFloat64 = 3 };
 enum { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
 enum { kCopy = 0, kReduce = 1 };
 
-constexpr int kMaxKSegs = 12; // 4 user segments x (head, body, tail)
+constexpr int kMaxKSegs = 48; // 16 user segments x (head, body, tail); 2.3 KB of kernarg
 constexpr int kTileVecs = 512; // 16-byte vectors per workgroup tile (256 threads x 2)
 
 struct KSeg {

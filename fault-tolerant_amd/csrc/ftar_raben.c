@@ -80,6 +80,41 @@ static void rb_windows(int v, size_t count, int steps, int64_t *rindex, int64_t 
 
 static void *at(const rb_ctx *x, void *base, int64_t idx) { return (char *)base + (size_t)idx * x->es; }
 
+static int rb_vrank_of(const rb_ctx *x, int cr)
+{
+    if (cr < 2 * x->rem) return (cr % 2 == 0) ? cr / 2 : -1;
+    return cr - x->rem;
+}
+
+/* Every receiver's pull(s) at a reduce-scatter (ag = 0) or allgather (ag = 1) step:
+ * what ftar_xfer needs to stripe the exchange over relays (raben/rabenseifner.c:170-249,
+ * :299-315). */
+static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
+{
+    ftar_comm *c = x->c;
+    ftar_plan_clear(P);
+    int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
+    for (int cr = 0; cr < c->size; cr++) {
+        int v = rb_vrank_of(x, cr);
+        if (v == -1) continue;
+        rb_windows(v, x->count, x->steps, ri, si, rc, sc);
+        int src = c->order[rb_real(x, v ^ mask)];
+        ftar_pull *pl = P->pull[cr];
+        memset(pl, 0, sizeof(ftar_pull) * FTAR_MAX_PULLS);
+        if (ag) {
+            pl[0] = (ftar_pull){FDEV_COPY, 0, src, WS_W, WS_W, WS_W, si[step], sc[step]};
+            P->npull[cr] = 1;
+        } else if (step == 0) {
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, WS_IN, ri[0], rc[0]};
+            pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0]};
+            P->npull[cr] = 2;
+        } else {
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_W, WS_W, WS_W, ri[step], rc[step]};
+            P->npull[cr] = 1;
+        }
+    }
+}
+
 static void run_reduce(rb_ctx *x, void *out, const void *xin, const void *yin, int64_t n, int remote, int tag)
 {
     fdev_seg s = {FDEV_REDUCE, remote, out, xin, yin, (size_t)n};
@@ -265,69 +300,69 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     /* ---- reduce-scatter (:170-284) ---- */
     int step = 0;
     for (int mask = 1; mask < x->adjsize; mask <<= 1, step++) {
+        ftar_plan P;
+        ftar_xstate xs;
+        memset(&xs, 0, sizeof(xs));
+        rb_plan(x, step, mask, 0, &P);
+        ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BEFORE);
+        int skip = 0;
         if (x->vrank != -1) {
-            ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BEFORE);
             int pw = c->order[rb_real(x, x->vrank ^ mask)];
-            if (ftar_is_dead(c, pw)) {
-                x->corr = 1; /* the exchange failed (:238-241) */
-            } else if (step == 0) {
-                /* :206-211 full exchange + :231-237 reduce.  The reduce half is on the
-                 * critical path; the redundancy half (kept in T for recovery, :191-197) is
-                 * only needed by a later error handler, so it runs on the background stream
-                 * and overlaps steps 1.. (joined before any replay and before the final
-                 * barrier).  FTAR_OVERLAP=0 keeps both halves in one launch. */
-                void *PIN = ftar_buf(c, pw, WS_IN);
-                fdev_seg s[2] = {
-                    {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, x->rindex[0]), at(x, IN, x->rindex[0]),
-                     at(x, PIN, x->rindex[0]), (size_t)x->rcount[0]},
-                    {FDEV_COPY, FDEV_REMOTE_X, at(x, T, x->sindex[0]), at(x, PIN, x->sindex[0]), NULL,
-                     (size_t)x->scount[0]},
-                };
-                if (c->overlap) {
-                    ftar_run(c, x->dtype, x->op, &s[0], 1, FDEV_TAG_STEP0);
-                    ftar_run_bg(c, x->dtype, x->op, &s[1], 1, FDEV_TAG_BG);
-                    x->bg_pending = 1;
-                    c->stats.step0_link_bytes = (double)x->rcount[0] * (double)x->es;
-                } else {
-                    ftar_run(c, x->dtype, x->op, s, 2, FDEV_TAG_STEP0);
-                    c->stats.step0_link_bytes = (double)count * (double)x->es;
-                }
-                ftar_drain(c);
-            } else {
-                void *PW = ftar_buf(c, pw, WS_W);
-                run_reduce(x, at(x, W, x->rindex[step]), at(x, W, x->rindex[step]), at(x, PW, x->rindex[step]),
-                           x->rcount[step], FDEV_REMOTE_Y, FDEV_TAG_STEP);
+            if (ftar_is_dead(c, pw)) skip = x->corr = 1; /* the exchange failed (:238-241) */
+            c->stats.steps++;
+        }
+        double lb0 = ftar_link_bytes(c);
+        int tag = step == 0 ? FDEV_TAG_STEP0 : FDEV_TAG_STEP;
+        if (step == 0 && c->overlap && !ftar_xfer_would_relay(c, &P, x->es)) {
+            /* :206-211 full exchange + :231-237 reduce, direct.  The reduce half is on the
+             * critical path; the redundancy half (kept in T for recovery, :191-197) is only
+             * needed by a later error handler, so it runs on the background stream and
+             * overlaps steps 1.. (joined before any replay and before the final barrier).
+             * (With relays both halves are striped in the step itself.) */
+            if (x->vrank != -1 && !skip) {
+                const ftar_pull *pl = P.pull[x->rank];
+                void *PIN = ftar_buf(c, pl[0].src, WS_IN);
+                fdev_seg s0 = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, pl[0].off), at(x, IN, pl[0].off),
+                               at(x, PIN, pl[0].off), (size_t)pl[0].n};
+                fdev_seg s1 = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
+                               (size_t)pl[1].n};
+                ftar_run(c, x->dtype, x->op, &s0, 1, FDEV_TAG_STEP0);
+                ftar_run_bg(c, x->dtype, x->op, &s1, 1, FDEV_TAG_BG);
+                x->bg_pending = 1;
                 ftar_drain(c);
             }
-            c->stats.steps++;
             ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_AFTER);
         } else {
-            ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BEFORE);
-            ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_AFTER);
+            ftar_xfer_step(c, &P, x->dtype, x->op, tag, skip, FTAR_PH_LOOP, step, &xs);
         }
+        if (step == 0) c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
         ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BARRIER);
         uint64_t newf = ftar_step_sync(c, 2 * x->steps); /* agree + barrier (:258-265) */
-        if (newf) rb_handler_rs(x, newf, step);
+        if (newf) {
+            ftar_xfer_repair(c, &P, x->dtype, x->op, &xs, newf);
+            rb_handler_rs(x, newf, step);
+        }
     }
 
     /* ---- allgather (:299-355) ---- */
     step = x->steps - 1;
     for (int mask = x->adjsize >> 1; mask > 0; mask >>= 1, step--) {
+        ftar_plan P;
+        ftar_xstate xs;
+        rb_plan(x, step, mask, 1, &P);
         ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BEFORE);
+        int skip = 0;
         if (x->vrank != -1) {
-            int pw = c->order[rb_real(x, x->vrank ^ mask)];
-            if (!ftar_is_dead(c, pw)) {
-                void *PW = ftar_buf(c, pw, WS_W);
-                run_copy(x, at(x, W, x->sindex[step]), at(x, PW, x->sindex[step]), x->scount[step], FDEV_REMOTE_X,
-                         FDEV_TAG_STEP);
-                ftar_drain(c);
-            }
+            skip = ftar_is_dead(c, c->order[rb_real(x, x->vrank ^ mask)]);
             c->stats.steps++;
         }
-        ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_AFTER);
+        ftar_xfer_step(c, &P, x->dtype, x->op, FDEV_TAG_STEP, skip, FTAR_PH_AG, step, &xs);
         ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BARRIER);
         uint64_t newf = ftar_step_sync(c, 2 * x->steps); /* (:330-335) */
-        if (newf) rb_handler_ag(x, newf, step);
+        if (newf) {
+            ftar_xfer_repair(c, &P, x->dtype, x->op, &xs, newf);
+            rb_handler_ag(x, newf, step);
+        }
     }
 
     if (x->bg_pending) { /* peers read our IN until their copies are done: join before the barrier */

@@ -218,26 +218,42 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     for (int distance = 1; distance < x->nactive; distance *= 2, iter++) {
         int last = (distance * 2 >= x->nactive);
         int i = index_of(x->active, x->nactive, me);
-        ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BEFORE);
-        if (i >= 0) {
-            int pw = x->active[i ^ distance];
-            if (!ftar_is_dead(c, pw)) {
-                int out = (x->cur == WS_W) ? WS_T : WS_W;
-                const void *A = c->ws[x->cur];
-                const void *PA = ftar_buf(c, pw, peer_cur(x, pw));
-                int tag = (iter == 0) ? FDEV_TAG_STEP0 : FDEV_TAG_STEP;
-                if (last) run1(x, FDEV_REDUCE, c->ws[out], PA, A, FDEV_REMOTE_X, tag); /* dst = src + dst */
-                else run1(x, FDEV_REDUCE, c->ws[out], A, PA, FDEV_REMOTE_Y, tag);      /* src = dst + src */
-                ftar_drain(c);
-                x->cur = out;
-                publish_cur(x);
+        int out = (x->cur == WS_W) ? WS_T : WS_W;
+        /* every active rank's pull (ftar_xfer stripes it over relays when large):
+         * middle steps src = dst + src (:48, Reduce_local(dst, src)), last step
+         * dst = src + dst (:44, Reduce_local(src, dst)) -- the pulled operand first */
+        ftar_plan P;
+        ftar_xstate xs;
+        ftar_plan_clear(&P);
+        for (int a = 0; a < x->nactive; a++) {
+            int cr = ftar_comm_rank_of(c, x->active[a]);
+            int pw = x->active[a ^ distance];
+            ftar_pull *pl = &P.pull[cr][0];
+            *pl = (ftar_pull){FDEV_REDUCE, last, pw, peer_cur(x, pw), 0, 0, 0, (int64_t)count};
+            if (a == i) {
+                pl->dst_buf = out;
+                pl->x_buf = x->cur;
             }
+            P.npull[cr] = 1;
+        }
+        ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BEFORE);
+        int skip = 0;
+        if (i >= 0) {
+            skip = ftar_is_dead(c, x->active[i ^ distance]); /* corrupted (:35-49 ignore the error) */
             c->stats.steps++;
         }
-        ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_AFTER);
+        double lb0 = ftar_link_bytes(c);
+        ftar_xfer_step(c, &P, x->dtype, x->op, iter == 0 ? FDEV_TAG_STEP0 : FDEV_TAG_STEP, skip, FTAR_PH_LOOP, iter,
+                       &xs);
+        if (iter == 0) c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
+        if (i >= 0 && !skip) {
+            x->cur = out;
+            publish_cur(x);
+        }
         ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BARRIER);
         newf = ftar_step_sync(c, ftar_hibit(x->nactive, 31) > 0 ? ftar_hibit(x->nactive, 31) : 1); /* (:51-53) */
         if (newf) {
+            ftar_xfer_repair(c, &P, x->dtype, x->op, &xs, newf);
             int dd = rd_handler(x, newf, distance * 2);
             distance = dd / 2;
         }

@@ -169,6 +169,7 @@ typedef struct {
     double sync_wait_s;      /* host time spent in agree/barrier rounds */
     double drain_s;          /* host time spent waiting for the device stream */
     int    syncs;            /* agree/barrier rounds */
+    int    relayed_steps;    /* exchange steps striped over 2-hop relays */
 } ftar_stats;
 
 int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);

@@ -18,9 +18,9 @@ import pytest
 import harness as H
 
 
-def _cmp(oracle_fn, algo, inputs, kills=(), op=0):
+def _cmp(oracle_fn, algo, inputs, kills=(), op=0, env=None):
     o = oracle_fn(inputs, kills, op=op)
-    r = H.run_probe(algo, inputs, kills, op=op, backend="hostsim", timeout=120)
+    r = H.run_probe(algo, inputs, kills, op=op, backend="hostsim", timeout=120, env_extra=env)
     u = {4: np.uint32, 8: np.uint64}[inputs[0].dtype.itemsize]
     if o.aborted:
         assert r.aborted and not r.outputs, (kills, r.stderr[-1000:])
@@ -173,3 +173,47 @@ def test_random_external_kill_never_wrong(hostsim, oracle, seed):
     if not aborted:
         assert len(hello) >= n - 1
     subprocess.run(f"rm -f /dev/shm/ftarhs-ext{seed}-*", shell=True)
+
+
+RELAY_ALL = {"FTAR_RELAY_MIN": "0"}
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [3, 4, 5, 6, 8, 9])
+def test_relay_nofault_parity(hostsim, oracle, algo, p):
+    """Exchanges striped over 2-hop relays give bit-identical results."""
+    o, r = _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 5003, seed=p), env=RELAY_ALL)
+    relayed = [st[0][8] for st in r.status.values()]
+    nrecv = p if algo == "raben" and p & (p - 1) == 0 else (1 << (p.bit_length() - 1))
+    if nrecv >= 3:
+        assert min(relayed) > 0, relayed
+
+
+@pytest.mark.parametrize("algo,p", [("raben", 5), ("raben", 9), ("rd", 4), ("rd", 8), ("rd", 6)])
+def test_relay_single_kill_sweep(hostsim, oracle, algo, p):
+    """Relays that die before or after forwarding, partners that die mid-step: same
+    outcomes and bits as the oracle (lost stripes are re-pulled before the handler)."""
+    ins = oracle.random_inputs(p, 3001, seed=p + 1)
+    fn = _fn(oracle, algo)
+    phases = [1, 2] if algo == "raben" else [1]
+    n = 0
+    for v in range(p):
+        for ph in phases:
+            for st in range(3):
+                for pt in range(3):
+                    ks = [(v, ph, st, pt)]
+                    if fn(ins, ks).status[v] != oracle.DEAD:
+                        continue
+                    _cmp(fn, algo, ins, ks, env=RELAY_ALL)
+                    n += 1
+    assert n > 0
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_relay_multi_kill_random(hostsim, oracle, seed):
+    rng = random.Random(100 + seed)
+    algo = rng.choice(["raben", "rd"])
+    p = rng.choice([6, 7, 9, 11])
+    victims = rng.sample(range(p), rng.choice([1, 2]))
+    kills = [(v, rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(3), rng.randrange(3)) for v in victims]
+    _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 2049, seed=seed), kills, env=RELAY_ALL)
