@@ -194,6 +194,7 @@ def multi(args):
 
     t_rb, k_rb = timed(raben)
     step0_bytes = timed.link_bytes
+    relayed = comm.last_stats().relayed_steps > 0
     # correctness spot check against torch.distributed's all_reduce on the same inputs
     # (fp32, different reduction order: |err| <= log2(p) * 2^-24 * sum|x_i|)
     ref = x.clone() if args.dist_backend == "nccl" else x.cpu()
@@ -201,6 +202,21 @@ def multi(args):
     raben()
     err = (y.cpu() - ref.cpu()).abs().max().item()
     t_rd, k_rd = timed(rd)
+    # the same schedules over plain pairwise exchanges (one link per step), with and
+    # without the background-stream redundancy copy -- the reference's transport shape
+    transports = {}
+    if not args.no_variants:
+        defaults = {o: comm.get_option(o) for o in (ftar.OPT_RELAY, ftar.OPT_OVERLAP)}
+        for name, relay, overlap in (("direct", 0, 1), ("direct_serial", 0, 0)):
+            comm.set_option(ftar.OPT_RELAY, relay)
+            comm.set_option(ftar.OPT_OVERLAP, overlap)
+            tv, _ = timed(raben)
+            tv_rd, _ = timed(rd) if name == "direct" else (None, None)
+            transports[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2)}
+            if tv_rd:
+                transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
+        for o, v in defaults.items():
+            comm.set_option(o, v)
     # end-to-end with host buffers: pinned H2D + device Allreduce + D2H (never the value)
     xh = x.cpu().pin_memory()
     yh = torch.empty_like(xh).pin_memory()
@@ -222,14 +238,22 @@ def multi(args):
 
         t_nc, _ = timed(rccl)
     L = world.bit_length() - 1
-    pow2 = (1 << L) == world
-    # link bytes per rank per direction on the critical path (SURVEY.md 8d counts the
-    # step-0 full exchange, (2.5 - 2^(1-L)) S; with the redundancy half overlapped on the
-    # background stream the critical path carries 2 (1 - 2^-L) S, classic Rabenseifner)
-    link_bytes_raben = ((2.5 - 2.0 ** (1 - L)) * S if os.environ.get("FTAR_OVERLAP", "1") == "0"
-                        else 2 * (1 - 2.0 ** -L) * S) if pow2 else None
-    t_roof = link_bytes_raben / (XGMI_LINK_GBS * 1e9) if link_bytes_raben else None
-    achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernel's pulled bytes
+    r = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
+    # Link bytes per rank per direction on the critical path: the FT
+    # step-0 full exchange makes the schedule move (2.5 - 2^(1-L)) S; with the redundancy
+    # half on the background stream the critical path of a direct transport carries
+    # 2 (1 - 2^-L) S on one link per step.  A relayed step moves 2/(r-1) of its window
+    # per link (two phases over r-1 links).
+    ft_bytes = (2.5 - 2.0 ** (1 - L)) * S
+    if relayed:
+        t_roof = 2.0 / (r - 1) * ft_bytes / (XGMI_LINK_GBS * 1e9)
+    elif os.environ.get("FTAR_OVERLAP", "1") != "0":
+        t_roof = 2 * (1 - 2.0 ** -L) * S / (XGMI_LINK_GBS * 1e9)
+    else:
+        t_roof = ft_bytes / (XGMI_LINK_GBS * 1e9)
+    links = (r - 1) if relayed else 1
+    peak = links * XGMI_LINK_GBS
+    achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernels' pulled bytes
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(world * S / t_rb / 1e9, 2), "unit": "GB/s", "n_gpus": world,
@@ -240,19 +264,22 @@ def multi(args):
                                    "rank, one rank per MI355X, pull exchanges over xGMI",
                        "count": args.count, "parallelism": f"{world} ranks"},
             "algbw_GBps": round(S / t_rb / 1e9, 2),
-            "schedule_link_roofline": {"bytes_per_rank_per_direction": link_bytes_raben, "link_GBps": XGMI_LINK_GBS,
-                                       "t_roof_ms": round(t_roof * 1e3, 3) if t_roof else None,
-                                       "frac": round(t_roof / t_rb, 4) if t_roof else None},
+            "transport": "relay2hop" if relayed else "direct",
+            "schedule_link_roofline": {"ft_schedule_bytes_per_rank": ft_bytes, "link_GBps": XGMI_LINK_GBS,
+                                       "links_per_step": links, "t_roof_ms": round(t_roof * 1e3, 3),
+                                       "frac": round(t_roof / t_rb, 4)},
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
-                         "peak": XGMI_LINK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / XGMI_LINK_GBS, 4) if achieved else None, "traffic": None,
-                         "kernel": "Raben RS step 0 reduce half (pull partner's half, reduce into W)",
+                         "peak": peak, "unit": "GB/s",
+                         "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
+                         "kernel": ("Raben RS step 0, both relay phases (stripes pulled over r-1 links)" if relayed
+                                    else "Raben RS step 0 reduce half (pull partner's half, reduce into W)"),
                          "algorithmic_bytes_per_launch": step0_bytes, "kernel_ms": round(k_rb, 4)},
             "e2e_host_buffers": {"ms_per_step": round(t_e2e * 1e3, 3), "algbw_GBps": round(S / t_e2e / 1e9, 2)},
             "rd": {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
                    "step0_kernel_ms": round(k_rd, 4)},
             "rccl_allreduce": ({"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2)}
                                if t_nc else None),
+            "transports": transports,
             "max_abs_err_vs_rccl": err,
             "cpu_baseline": None,
         }
@@ -269,6 +296,7 @@ def main():
     ap.add_argument("--count", type=int, default=COUNT)
     ap.add_argument("--variant", type=int, default=0, help="local-reduce kernel: 0 register, 1 LDS-DMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="N>1: skip the direct-transport comparison")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for barrier/timing")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -24,6 +24,7 @@ INT32, FLOAT32, INT64, FLOAT64 = 0, 1, 2, 3
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
 PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
 PT_BEFORE, PT_AFTER, PT_BARRIER = 0, 1, 2
+OPT_OVERLAP, OPT_RELAY, OPT_RELAY_MIN, OPT_LOOP_SECONDS = 0, 1, 2, 3
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
 
 
@@ -81,6 +82,8 @@ def lib():
         "ftar_reduce_local": ([vp, vp, sz, i, i, vp], i),
         "ftar_set_reduce_variant": ([i], i),
         "ftar_comm_set_stream": ([vp, vp], i),
+        "ftar_comm_set_option": ([vp, i, ctypes.c_double], i),
+        "ftar_comm_get_option": ([vp, i, ctypes.POINTER(ctypes.c_double)], i),
         "ftar_last_stats": ([vp, ctypes.POINTER(Stats)], i),
         "ftar_set_profiling": ([vp, i], i),
         "ftar_version": ([], ctypes.c_char_p),
@@ -181,6 +184,15 @@ class Comm:
 
     def set_stream(self, stream):
         _check(lib().ftar_comm_set_stream(self._h, stream), "ftar_comm_set_stream")
+
+    def set_option(self, opt: int, value: float):
+        """Transport option (collective: same value on every live rank before the next call)."""
+        _check(lib().ftar_comm_set_option(self._h, opt, float(value)), "ftar_comm_set_option")
+
+    def get_option(self, opt: int) -> float:
+        v = ctypes.c_double()
+        _check(lib().ftar_comm_get_option(self._h, opt, ctypes.byref(v)), "ftar_comm_get_option")
+        return v.value
 
     def set_profiling(self, on: bool):
         _check(lib().ftar_set_profiling(self._h, int(on)), "ftar_set_profiling")

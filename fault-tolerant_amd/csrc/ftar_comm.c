@@ -126,7 +126,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->loop_seconds = getenv("FTAR_LOOP_SECONDS") ? atof(getenv("FTAR_LOOP_SECONDS")) : 0.0;
     c->overlap = getenv("FTAR_OVERLAP") ? atoi(getenv("FTAR_OVERLAP")) : 1;
     c->relay = getenv("FTAR_RELAY") ? atoi(getenv("FTAR_RELAY")) : 1;
-    c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)1 << 20);
+    c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)4 << 20);
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
     if (rc) {
@@ -253,6 +253,32 @@ int ftar_comm_set_stream(ftar_comm *c, void *stream)
 {
     if (!c) return FTAR_ERR_ARG;
     c->user_stream = stream;
+    return FTAR_SUCCESS;
+}
+
+int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
+{
+    if (!c || v < 0) return FTAR_ERR_ARG;
+    switch (opt) {
+    case FTAR_OPT_OVERLAP: c->overlap = v != 0; break;
+    case FTAR_OPT_RELAY: c->relay = v != 0; break;
+    case FTAR_OPT_RELAY_MIN: c->relay_min = (size_t)v; break;
+    case FTAR_OPT_LOOP_SECONDS: c->loop_seconds = v; break;
+    default: return FTAR_ERR_ARG;
+    }
+    return FTAR_SUCCESS;
+}
+
+int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
+{
+    if (!c || !v) return FTAR_ERR_ARG;
+    switch (opt) {
+    case FTAR_OPT_OVERLAP: *v = c->overlap; break;
+    case FTAR_OPT_RELAY: *v = c->relay; break;
+    case FTAR_OPT_RELAY_MIN: *v = (double)c->relay_min; break;
+    case FTAR_OPT_LOOP_SECONDS: *v = c->loop_seconds; break;
+    default: return FTAR_ERR_ARG;
+    }
     return FTAR_SUCCESS;
 }
 

@@ -153,6 +153,18 @@ int ftar_set_reduce_variant(int variant);
 /* Stream the comm orders its work after (hipStream_t, NULL = null stream). */
 int ftar_comm_set_stream(ftar_comm *comm, void *stream);
 
+/* Transport options (defaults come from the FTAR_* environment at init).  Collective:
+ * every live rank of the comm must set the same value before its next call. */
+typedef enum {
+    FTAR_OPT_OVERLAP = 0,      /* Raben step-0 redundancy copy on a background stream (0/1) */
+    FTAR_OPT_RELAY = 1,        /* stripe exchanges over 2-hop relay paths (0/1) */
+    FTAR_OPT_RELAY_MIN = 2,    /* smallest window, in bytes, that is relayed */
+    FTAR_OPT_LOOP_SECONDS = 3  /* stretch of the step loop for fault-injection runs */
+} ftar_option;
+
+int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);
+int ftar_comm_get_option(const ftar_comm *comm, ftar_option opt, double *value);
+
 /* ---- statistics of the last allreduce call on this rank ----------------- */
 typedef struct {
     int    steps;            /* exchange steps executed (pre/loop/allgather/post) */

@@ -1,0 +1,97 @@
+"""Compare campaign: run/run_compare.sh -> ftrun -> drivers ->
+analysis/check_compare.py -> data_compare CSVs (the reference's slurm/test_compare.slurm +
+analysis/check_compare.py layout)."""
+import csv
+import importlib.util
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "fault-tolerant_amd")
+RUN = os.path.join(PKG, "run")
+
+
+def _checker(out, data):
+    os.environ["FTAR_CMP_OUT"], os.environ["FTAR_CMP_DATA"] = str(out), str(data)
+    try:
+        spec = importlib.util.spec_from_file_location("check_compare", os.path.join(PKG, "analysis", "check_compare.py"))
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+    finally:
+        del os.environ["FTAR_CMP_OUT"], os.environ["FTAR_CMP_DATA"]
+    return m
+
+
+def _stdout(np_, size, t, results, header_on_all=False):
+    lines = []
+    for r, v in enumerate(results):
+        if header_on_all or r == 0:
+            lines += [f"P: {np_}", f"Size: {size}", f"Time: {t:f}"]
+        lines.append(f"Hello from {r} of {np_} and the result is: {v}")
+    return "\n".join(lines) + "\n"
+
+
+def _rows(path):
+    return list(csv.DictReader(open(path), delimiter=";"))
+
+
+def test_check_compare_rows_and_errors(tmp_path):
+    out, data = tmp_path / "out", tmp_path / "data"
+    out.mkdir()
+    m = _checker(out, data)
+    good = ((4 * 3 // 2) % 17) * 1000
+    (out / "rd.txt").write_text(_stdout(4, 1000, 0.25, [good] * 4, header_on_all=True))
+    (out / "original_rd.txt").write_text(_stdout(4, 1000, 0.125, [good] * 4))
+    (out / "raben.txt").write_text(_stdout(4, 1000, 0.5, [good] * 3 + [good + 1], header_on_all=True))
+    (out / "original_raben.txt").write_text(_stdout(4, 1000, 0.1, [good] * 4))
+    assert m.main() == 1
+    assert _rows(data / "rd.csv") == [{"NP": "4", "SIZE": "1000", "TIME": "0.25", "RESULT": str(good)}]
+    assert _rows(data / "original_rd.csv")[0]["TIME"] == "0.125"
+    assert not (data / "raben.csv").exists() and not (data / "original_raben.csv").exists()
+    err = (out / "error.txt").read_text()
+    assert err.startswith("RABEN: [4, 1000, 0.5,") and "RABEN_O: [4, 1000, 0.1," in err
+    # a missing rank (fewer Hello lines than P) is an error as in the reference
+    (out / "raben.txt").write_text(_stdout(4, 1000, 0.5, [good] * 3, header_on_all=True))
+    assert m.check_pair("raben", "original_raben", "RABEN") is False
+    (out / "raben.txt").write_text(_stdout(4, 1000, 0.5, [good] * 4, header_on_all=True))
+    assert m.check_pair("raben", "original_raben", "RABEN") is True
+    assert len(_rows(data / "raben.csv")) == 1 and len(_rows(data / "rd.csv")) == 1
+
+
+def test_run_compare_campaign_hostsim(hostsim, tmp_path):
+    """The campaign loop end to end on CPU: host-sim FT drivers in all four slots (the
+    vendor baseline needs RCCL on a GPU; it runs in the GPU test below)."""
+    hs = os.path.join(ROOT, "tests", "hostsim", "_build", "src")
+    env = dict(os.environ, FTAR_CMP_NPS="3 4", FTAR_CMP_BUF_MIN="1", FTAR_CMP_BUF_MAX="64",
+               FTAR_CMP_RD=f"{hs}/rd/main", FTAR_CMP_RABEN=f"{hs}/raben/main",
+               FTAR_CMP_ORIG_RD=f"{hs}/rd/main", FTAR_CMP_ORIG_RABEN=f"{hs}/raben/main",
+               FTAR_CMP_OUT=str(tmp_path / "out"), FTAR_CMP_DATA=str(tmp_path / "data"),
+               FTAR_HOSTSIM_TAG="compare")
+    os.makedirs(tmp_path / "out")
+    cp = subprocess.run(["./run_compare.sh", "1"], cwd=RUN, env=env, capture_output=True, text=True, timeout=300)
+    subprocess.run("rm -f /dev/shm/ftarhs-compare-*", shell=True)
+    assert cp.returncode == 0, cp.stdout[-2000:] + cp.stderr[-2000:]
+    for name in ("rd", "original_rd", "raben", "original_raben"):
+        rows = _rows(tmp_path / "data" / f"{name}.csv")
+        assert len(rows) == 2 * 7, (name, rows)
+        for r in rows:
+            n, size = int(r["NP"]), int(r["SIZE"])
+            assert int(r["RESULT"]) == ((n * (n - 1) // 2) % 17) * size
+    assert not (tmp_path / "out" / "error.txt").exists()
+
+
+@pytest.mark.gpu
+def test_run_compare_campaign_gpu(tmp_path):
+    """All four executables on the GPU (NP = 1: the box has one GPU and RCCL refuses two
+    ranks on one device), including the RCCL vendor baseline."""
+    env = dict(os.environ, FTAR_CMP_NPS="1", FTAR_CMP_BUF_MIN="1", FTAR_CMP_BUF_MAX="65536",
+               FTAR_CMP_OUT=str(tmp_path / "out"), FTAR_CMP_DATA=str(tmp_path / "data"))
+    os.makedirs(tmp_path / "out")
+    cp = subprocess.run(["./run_compare.sh", "1"], cwd=RUN, env=env, capture_output=True, text=True, timeout=600)
+    assert cp.returncode == 0, cp.stdout[-2000:] + cp.stderr[-2000:]
+    for name in ("rd", "original_rd", "raben", "original_raben"):
+        rows = _rows(tmp_path / "data" / f"{name}.csv")
+        assert len(rows) == 17, (name, rows, cp.stdout[-2000:])
+        assert all(int(r["RESULT"]) == 0 for r in rows)

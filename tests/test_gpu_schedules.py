@@ -19,9 +19,10 @@ pytestmark = pytest.mark.gpu
 ALL_ON_GPU0 = ",".join(["0"] * 16)
 
 
-def _check(oracle_fn, algo, inputs, kills=(), op=0, iters=1):
+def _check(oracle_fn, algo, inputs, kills=(), op=0, iters=1, env=None):
     o = oracle_fn(inputs, kills, op=op)
-    r = H.run_probe(algo, inputs, kills, op=op, iters=iters, backend="gpu", devmap=ALL_ON_GPU0, timeout=300)
+    r = H.run_probe(algo, inputs, kills, op=op, iters=iters, backend="gpu", devmap=ALL_ON_GPU0, timeout=300,
+                    env_extra=env)
     u = {4: np.uint32, 8: np.uint64}[inputs[0].dtype.itemsize]
     if o.aborted:
         assert r.aborted, r.stderr[-2000:]
@@ -111,3 +112,24 @@ def test_driver_checksums(oracle):
         assert sorted(hello) == [0, 1, 2, 3]
         assert set(hello.values()) == {oracle.expected_checksum(4, 100000)}
         assert "P: 4" in cp.stdout and "Size: 100000" in cp.stdout and "Time:" in cp.stdout
+
+
+RELAY_ALL = {"FTAR_RELAY_MIN": "0"}
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [4, 6, 8, 9])
+def test_relay_nofault(oracle, algo, p):
+    """Exchanges striped over 2-hop relays (forced on for every window size)."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    o, r = _check(fn, algo, oracle.random_inputs(p, 100003, seed=p + 20), env=RELAY_ALL)
+    assert min(st[0][8] for st in r.status.values()) > 0
+
+
+@pytest.mark.parametrize("algo,kill", [("raben", (5, 1, 1, 1)), ("raben", (3, 1, 2, 1)), ("raben", (4, 2, 1, 1)),
+                                       ("raben", (6, 1, 1, 2)), ("rd", (2, 1, 1, 1)), ("rd", (5, 1, 0, 1))])
+def test_relay_kill(oracle, algo, kill):
+    """A rank killed right after its relay phase: lost stripes are re-pulled directly."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    p = 9 if algo == "raben" else 8
+    _check(fn, algo, oracle.random_inputs(p, 65536 + 7, seed=30), [kill], env=RELAY_ALL)
