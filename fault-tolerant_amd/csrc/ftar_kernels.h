@@ -12,6 +12,8 @@ enum { kCopy = 0, kReduce = 1 };
 
 constexpr int kMaxKSegs = 48; // 16 user segments x (head, body, tail); 2.3 KB of kernarg
 constexpr int kTileVecs = 512; // 16-byte vectors per workgroup tile (256 threads x 2)
+constexpr int kChunkTiles = 8; // tiles per chunk of the interleaved block mapping (64 KiB)
+constexpr int kMaxIleave = 16; // vector pieces that can share the interleaved prefix
 
 struct KSeg {
     void *out;
@@ -20,13 +22,22 @@ struct KSeg {
     size_t n;
     unsigned kind;
     unsigned vec;
-    unsigned blk_begin;
+    unsigned blk_begin;  // sequential region: blocks [blk_begin, blk_end) ...
     unsigned blk_end;
+    unsigned tile_base;  // ... take tiles tile_base, tile_base + 1, ... of this piece
+    unsigned ntiles;     // tiles of the whole piece (the stride of a capped grid)
 };
 
+// Blocks [0, il_blocks) are dealt round-robin, one kChunkTiles chunk at a time, over the
+// vector pieces il[0..nil): pieces that pull from different peers then stream over
+// their xGMI links at the same time instead of one after the other.  The remaining
+// blocks map sequentially (blk_begin/blk_end) onto what is left of every piece.
 struct KSegList {
     KSeg s[kMaxKSegs];
     int nseg;
+    int nil;
+    unsigned il_blocks;
+    unsigned char il[kMaxIleave];
 };
 
 struct SegIn {

@@ -79,12 +79,11 @@ __device__ __forceinline__ uint4 ldnt(const uint4 *p)
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-__device__ __forceinline__ int find_segment(const KSegList &L)
+__device__ __forceinline__ int find_segment(const KSegList &L, unsigned b)
 {
     // blockIdx is wave-uniform; readfirstlane keeps the search in SGPRs.
-    int b = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
     int si = 0;
-    while (si + 1 < L.nseg && (unsigned)b >= L.s[si].blk_end) si++;
+    while (si + 1 < L.nseg && b >= L.s[si].blk_end) si++;
     return __builtin_amdgcn_readfirstlane(si);
 }
 
@@ -137,12 +136,19 @@ __device__ __forceinline__ void scalar_body(const KSeg &S, size_t b, size_t nblk
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void segment_kernel(KSegList L)
 {
-    const int si = find_segment(L);
+    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    if (b < L.il_blocks) { // interleaved prefix: chunk q of piece il[q % nil]
+        const unsigned q = b / kChunkTiles;
+        const int si = __builtin_amdgcn_readfirstlane((int)L.il[q % (unsigned)L.nil]);
+        const KSeg &S = L.s[si];
+        vec_body<T, OP>(S, (size_t)(q / (unsigned)L.nil) * kChunkTiles + b % kChunkTiles, S.ntiles);
+        return;
+    }
+    const int si = find_segment(L, b);
     const KSeg &S = L.s[si];
-    const size_t nblk = S.blk_end - S.blk_begin;
-    const size_t b = blockIdx.x - S.blk_begin;
-    if (S.vec) vec_body<T, OP>(S, b, nblk);
-    else scalar_body<T, OP>(S, b, nblk);
+    const size_t j = b - S.blk_begin;
+    if (S.vec) vec_body<T, OP>(S, S.tile_base + j, S.tile_base ? S.ntiles : S.blk_end - S.blk_begin);
+    else scalar_body<T, OP>(S, j, S.blk_end - S.blk_begin);
 }
 
 // LDS-DMA staged local reduce (variant 1): the `in` operand is moved HBM -> LDS by
@@ -278,10 +284,53 @@ unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_bloc
         add(tail_off, g.n - tail_off, 0);
     }
     if (np == 0) return 0;
-    // blocks: a vector piece gets one block per tile of kBlock*kUnroll vectors (capped at
-    // max_blocks in total, pieces then loop); scalar pieces (heads/tails < 16 B, or
-    // non-co-aligned slow paths) get up to 64 blocks.
     const size_t tile_bytes = (size_t)kBlock * 16 * kUnroll;
+    size_t total_tiles = 0;
+    for (int i = 0; i < np; i++)
+        if (pieces[i].k.vec) total_tiles += (pieces[i].bytes + tile_bytes - 1) / tile_bytes;
+    L->nil = 0;
+    L->il_blocks = 0;
+    if (total_tiles + 64 * (size_t)np <= max_blocks) {
+        // uncapped grid: one block per tile.  Vector pieces of at least one chunk share
+        // an interleaved prefix of `rounds` chunks each (the shortest one's length).
+        size_t rounds = SIZE_MAX;
+        unsigned char il[kMaxIleave];
+        int nil = 0;
+        for (int i = 0; i < np && nil < kMaxIleave; i++) {
+            if (!pieces[i].k.vec) continue;
+            size_t t = (pieces[i].bytes + tile_bytes - 1) / tile_bytes;
+            if (t < (size_t)kChunkTiles) continue;
+            il[nil++] = (unsigned char)i;
+            if (t / kChunkTiles < rounds) rounds = t / kChunkTiles;
+        }
+        if (nil >= 2) {
+            L->nil = nil;
+            L->il_blocks = (unsigned)(rounds * kChunkTiles * nil);
+            memcpy(L->il, il, sizeof(il));
+        } else {
+            rounds = 0;
+        }
+        unsigned next = L->il_blocks;
+        for (int i = 0; i < np; i++) {
+            KSeg &k = pieces[i].k;
+            bool in_il = false;
+            for (int t = 0; t < L->nil; t++) in_il |= (L->il[t] == i);
+            size_t tiles = k.vec ? (pieces[i].bytes + tile_bytes - 1) / tile_bytes : 0;
+            size_t base = in_il ? rounds * kChunkTiles : 0;
+            size_t want = k.vec ? tiles - base : (k.n + kBlock - 1) / kBlock;
+            if (!k.vec && want > 64) want = 64;
+            k.ntiles = (unsigned)tiles;
+            k.tile_base = (unsigned)base;
+            k.blk_begin = next;
+            k.blk_end = next + (unsigned)want;
+            next = k.blk_end;
+            L->s[L->nseg++] = k;
+        }
+        return next;
+    }
+    // capped grid (more than max_blocks tiles): blocks split between the pieces in
+    // proportion to their bytes, pieces loop with a block stride; scalar pieces (heads/
+    // tails < 16 B, or non-co-aligned slow paths) get up to 64 blocks.
     unsigned next = 0;
     for (int i = 0; i < np; i++) {
         KSeg &k = pieces[i].k;
@@ -292,11 +341,14 @@ unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_bloc
                                                      (double)vec_bytes_total) + 1
                                            : 1;
             want = need < share ? need : share;
+            k.ntiles = (unsigned)need;
         } else {
             size_t need = (k.n + kBlock - 1) / kBlock;
             want = need < 64 ? need : 64;
+            k.ntiles = 0;
         }
         if (want < 1) want = 1;
+        k.tile_base = 0;
         k.blk_begin = next;
         k.blk_end = next + (unsigned)want;
         next = k.blk_end;

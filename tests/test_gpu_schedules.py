@@ -133,3 +133,16 @@ def test_relay_kill(oracle, algo, kill):
     fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
     p = 9 if algo == "raben" else 8
     _check(fn, algo, oracle.random_inputs(p, 65536 + 7, seed=30), [kill], env=RELAY_ALL)
+
+
+@pytest.mark.parametrize("algo,p,relay", [("raben", 8, True), ("rd", 8, True), ("raben", 9, False),
+                                          ("rd", 5, False)])
+def test_large_windows_interleaved(oracle, algo, p, relay):
+    """Windows of many 64 KiB chunks: multi-segment launches take the interleaved block
+    mapping (relay phases: up to 14 vector pieces from 7 peers; direct Raben step 0: the
+    reduce half and the copy half)."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    o, r = _check(fn, algo, oracle.random_inputs(p, (1 << 22) + 13, seed=p + 40),
+                  env=RELAY_ALL if relay else {"FTAR_RELAY": "0"})
+    if relay:
+        assert min(st[0][8] for st in r.status.values()) > 0
