@@ -66,6 +66,8 @@ struct ftar_dev {
     int device;
     hipStream_t stream;
     hipStream_t bg;
+    hipEvent_t fence_main; // system-scope release markers that sync_stream waits on
+    hipEvent_t fence_bg;
     int profiling;
     unsigned max_blocks;
     std::vector<Pending> pending;
@@ -103,6 +105,8 @@ int fdev_open(int device, ftar_dev **out)
     if (d->max_blocks == 0) d->max_blocks = 2048;
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&d->bg, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&d->fence_main, hipEventDisableTiming | hipEventReleaseToSystem));
+    HIPCHK(hipEventCreateWithFlags(&d->fence_bg, hipEventDisableTiming | hipEventReleaseToSystem));
     // Peer access to every other GPU of the node: the exchanges read peers' HBM.
     for (int p = 0; p < ndev; p++) {
         if (p == device) continue;
@@ -127,6 +131,8 @@ void fdev_close(ftar_dev *d)
         (void)hipEventDestroy(p.stop);
     }
     for (auto e : d->event_pool) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(d->fence_main);
+    (void)hipEventDestroy(d->fence_bg);
     (void)hipStreamDestroy(d->stream);
     (void)hipStreamDestroy(d->bg);
     delete d;
@@ -260,12 +266,20 @@ int fdev_order_after(ftar_dev *d, void *user_stream)
 
 static int harvest(ftar_dev *d);
 
+// Waits for everything enqueued on `st` by spinning on a system-scope release marker.
+// The marker is what makes a step's results visible to the peers that pull them next:
+// its release writes this GPU's dirty L2 lines back to HBM (peers read our HBM over
+// xGMI, not our L2) and its fence invalidates this GPU's cached copies of peer memory,
+// so the next step's pulls fetch the peers' new windows.  Without it the visibility of
+// a kernel's stores to other GPUs would depend on the runtime's default packet fences.
 static int sync_stream(ftar_dev *d, hipStream_t st, int (*poll)(void *), void *arg)
 {
+    hipEvent_t fence = st == d->bg ? d->fence_bg : d->fence_main;
+    HIPCHK(hipEventRecord(fence, st));
     for (;;) {
-        hipError_t e = hipStreamQuery(st);
+        hipError_t e = hipEventQuery(fence);
         if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) return set_err(e, "hipStreamQuery");
+        if (e != hipErrorNotReady) return set_err(e, "hipEventQuery");
         if (poll) {
             int r = poll(arg);
             if (r) return r;
