@@ -4,6 +4,9 @@
  *
  *   ftrun -np N [--devmap d0,d1,...] [--] prog [args...]
  *
+ * FTAR_PIN_CPUS=1 pins rank r to the r-th CPU of the launcher's affinity set (CPU
+ * baseline runs of the host-memory build: one process per core).
+ *
  * Creates the job's shared-memory control block, starts N rank processes (one per
  * GPU by default: rank r drives device r % ngpus, or devmap[r]), and reaps them.
  * The launcher itself never touches the GPU and sleeps in waitpid, so the harness's
@@ -16,6 +19,7 @@
 #define _GNU_SOURCE
 #endif
 #include <errno.h>
+#include <sched.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -118,6 +122,22 @@ int main(int argc, char **argv)
             if (dev[r] >= 0) {
                 snprintf(buf, sizeof(buf), "%d", dev[r]);
                 setenv("FTAR_DEVICE", buf, 1);
+            }
+            const char *pin = getenv("FTAR_PIN_CPUS");
+            if (pin && atoi(pin)) {
+                cpu_set_t all, one;
+                if (sched_getaffinity(0, sizeof(all), &all) == 0 && CPU_COUNT(&all) > 0) {
+                    int want = r % CPU_COUNT(&all), k = 0;
+                    for (int c = 0; c < CPU_SETSIZE; c++) {
+                        if (!CPU_ISSET(c, &all)) continue;
+                        if (k++ == want) {
+                            CPU_ZERO(&one);
+                            CPU_SET(c, &one);
+                            (void)sched_setaffinity(0, sizeof(one), &one);
+                            break;
+                        }
+                    }
+                }
             }
             execvp(argv[ai], &argv[ai]);
             fprintf(stderr, "ftrun: exec %s: %s\n", argv[ai], strerror(errno));

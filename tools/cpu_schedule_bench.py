@@ -1,0 +1,104 @@
+"""CPU baseline of the schedules: the build's own C host logic -- control
+plane, agree rounds, both FT schedules -- run as N host processes, one pinned per core,
+with POSIX shared memory as the transport and plain C loops as the reduce
+(tests/hostsim: the product's C sources linked against the host-memory device layer,
+built here with -O3 -march=native).  Reported beside the GPU numbers, never as them.
+
+    python tools/cpu_schedule_bench.py [--quick] [--out FILE]
+
+Configs: C1 (p = 4, 64 KiB int32, both schedules, the reference's driver case) and
+256 MiB float32 at p = 2 / 4 / 8 when the host has that many cores.  Time = the
+drivers' `Time:` line (wall clock of one call incl. copy-in/out), max over ranks,
+median over repetitions.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import resource
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HS = os.path.join(ROOT, "tests", "hostsim")
+OUT = "_build_o3"
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HS, f"OUT={OUT}", "CFLAGS=-O3 -march=native -g -std=c11 -Wall "
+                    "-Wno-unused-parameter -fPIC -D_GNU_SOURCE", f"{OUT}/src/rd/main", f"{OUT}/src/raben/main",
+                    f"{OUT}/bin/ftrun"], check=True)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def run(algo: str, p: int, count: int, dtype: str, reps: int) -> dict:
+    exe = os.path.join(HS, OUT, "src", algo, "main")
+    ftrun = os.path.join(HS, OUT, "bin", "ftrun")
+    env = dict(os.environ, FTAR_PIN_CPUS="1", FTAR_HOSTSIM_TAG=f"cpub{os.getpid()}", FTAR_DTYPE=dtype)
+    times, cpu = [], []
+    for _ in range(reps):
+        ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
+        cp = subprocess.run([ftrun, "-np", str(p), exe, str(count)], env=env, capture_output=True, text=True,
+                            timeout=600)
+        subprocess.run(f"rm -f /dev/shm/ftarhs-cpub{os.getpid()}-*", shell=True)
+        if cp.returncode != 0:
+            raise RuntimeError(f"{algo} p={p} failed: {cp.stderr[-1000:]}")
+        ts = [float(x) for x in re.findall(r"^Time: (\S+)", cp.stdout, flags=re.M)]
+        hello = re.findall(r"result is: (-?\d+)", cp.stdout)
+        expect = ((p * (p - 1) // 2) % 17) * count
+        if len(hello) != p or any(int(h) != expect for h in hello):
+            raise RuntimeError(f"{algo} p={p}: wrong checksums {hello} (expected {expect})")
+        times.append(max(ts))
+        ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+        cpu.append((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime) / p)
+    t = statistics.median(times)
+    S = count * 4
+    return {"algo": algo, "p": p, "count": count, "dtype": dtype, "reps": reps, "time_s": t,
+            "algbw_GBps": round(S / t / 1e9, 4), "times_s": times,
+            # the reference's TIME is clock() of one rank; ranks here spin, so CPU time per
+            # rank tracks wall time (this figure also covers init, fill and checksum)
+            "cpu_s_per_rank_whole_process": round(statistics.median(cpu), 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true", help="C1 only (seconds)")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    build()
+    ncpu = len(os.sched_getaffinity(0))
+    res = {"kind": "port (product host C + host-memory device layer, one process per core)",
+           "cpu_model": cpu_model(), "cpus": ncpu, "results": []}
+    t0 = time.time()
+    for algo in ("rd", "raben"):
+        res["results"].append(run(algo, 4, 16384, "int32", 20))
+    if not args.quick:
+        for p in (2, 4, 8):
+            if p > ncpu:
+                continue
+            for algo in ("rd", "raben"):
+                res["results"].append(run(algo, p, 67108864, "float32", 3))
+                print(json.dumps(res["results"][-1]), file=sys.stderr, flush=True)
+    res["wall_s"] = round(time.time() - t0, 1)
+    line = json.dumps(res)
+    print(line)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()

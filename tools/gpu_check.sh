@@ -48,4 +48,9 @@ if [[ $STEPS == *rehearse* ]]; then
     rc=$?; cat "$OUT/rehearse_$n.json"; tail -3 "$OUT/rehearse_$n.err"; stop_on_fault $rc rehearse_$n
   done
 fi
+if [[ $STEPS == *cpubase* ]]; then
+  # CPU baseline of the schedules on this box's host cores (no GPU involved)
+  timeout -k 10 900 python tools/cpu_schedule_bench.py --out "$OUT/cpu_schedule_bench.json" > "$OUT/cpubase.log" 2>&1
+  rc=$?; tail -c 600 "$OUT/cpu_schedule_bench.json"; stop_on_fault $rc cpubase
+fi
 echo ALLDONE
