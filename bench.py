@@ -201,6 +201,16 @@ def multi(args):
     dist.all_reduce(ref)
     raben()
     err = (y.cpu() - ref.cpu()).abs().max().item()
+    # the reference drivers' case (buffer[i] = rank, int32 SUM): closed-form checksum
+    # sum_i result[i] % 17 = ((p (p-1) / 2) % 17) * count  (analysis/check_fault.py:62-67)
+    xi = torch.full((args.count,), rank, dtype=torch.int32, device="cuda")
+    yi = torch.empty_like(xi)
+    assert comm.allreduce_rabenseifner(xi, yi) == 0
+    cks_raben = int((yi.to(torch.int64) % 17).sum().item())
+    assert comm.recursive_doubling(xi, yi) == 0
+    cks_rd = int((yi.to(torch.int64) % 17).sum().item())
+    cks_want = ((world * (world - 1) // 2) % 17) * args.count
+    del xi, yi
     t_rd, k_rd = timed(rd)
     # the same schedules over plain pairwise exchanges (one link per step), with and
     # without the background-stream redundancy copy -- the reference's transport shape
@@ -281,6 +291,7 @@ def multi(args):
                                if t_nc else None),
             "transports": transports,
             "max_abs_err_vs_rccl": err,
+            "int32_rank_checksum_ok": {"raben": cks_raben == cks_want, "rd": cks_rd == cks_want},
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)

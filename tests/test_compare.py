@@ -95,3 +95,42 @@ def test_run_compare_campaign_gpu(tmp_path):
         rows = _rows(tmp_path / "data" / f"{name}.csv")
         assert len(rows) == 17, (name, rows, cp.stdout[-2000:])
         assert all(int(r["RESULT"]) == 0 for r in rows)
+
+
+def _analyze():
+    spec = importlib.util.spec_from_file_location("ftar_analyze", os.path.join(PKG, "analysis", "analyze.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_analyze_compare_and_fault_tables(tmp_path):
+    a = _analyze()
+    ft, orig = tmp_path / "rd.csv", tmp_path / "original_rd.csv"
+    ft.write_text("NP;SIZE;TIME;RESULT\n4;16;0.2;96\n4;16;0.4;96\n4;32;0.5;192\n8;16;1.0;208\n")
+    orig.write_text("NP;SIZE;TIME;RESULT\n4;16;0.1;96\n4;32;0.25;192\n8;16;0.5;208\n8;64;1;0\n")
+    m = a.compare_table(str(ft), str(orig), "RD")
+    assert list(m["NP"]) == [4, 4, 8] and list(m["SIZE"]) == [16, 32, 16]
+    assert list(m["TIME_RD"].round(6)) == [0.3, 0.5, 1.0]
+    assert list(m["RATIO_RD"].round(6)) == [3.0, 2.0, 2.0]
+    log = tmp_path / "log.csv"
+    log.write_text("N;DELAY;BUF SIZE;KILLED;TIME;DEADLOCK;SEGFAULT;ABORT;RIGHT RESULT\n"
+                   "5;2;100;0;1.0;False;False;False;True\n5;2;100;0;3.0;False;False;False;True\n"
+                   "5;3;100;1;2.0;False;False;False;True\n5;3;100;1;31.0;True;False;False;False\n")
+    t = a.fault_table(str(log))
+    assert t.to_dict("records")[0]["count"] == 2 and t.to_dict("records")[0]["mean"] == 2.0
+    assert t.to_dict("records")[1]["count"] == 1 and t.to_dict("records")[1]["max"] == 2.0
+
+
+def test_analyze_clean_sampling(tmp_path):
+    a = _analyze()
+    src = tmp_path / "log.csv"
+    rows = ["N;KILLED;TIME"] + [f"{n};{k};{i}" for n in (5, 9) for k in (0, 1, 5) for i in range(80)]
+    src.write_text("\n".join(rows) + "\n")
+    kept = a.clean(str(src), str(tmp_path / "out.csv"), [5, 9])
+    assert kept == 4 * 50
+    out = _rows(tmp_path / "out.csv")
+    assert {(r["N"], r["KILLED"]) for r in out} == {("5", "0"), ("5", "1"), ("9", "0"), ("9", "1")}
+    # deterministic (seed 42 before every class pair, as clean_data.py)
+    a.clean(str(src), str(tmp_path / "out2.csv"), [5, 9])
+    assert (tmp_path / "out.csv").read_text() == (tmp_path / "out2.csv").read_text()
