@@ -216,12 +216,15 @@ def multi(args):
     # without the background-stream redundancy copy -- the reference's transport shape
     transports = {}
     if not args.no_variants:
-        defaults = {o: comm.get_option(o) for o in (ftar.OPT_RELAY, ftar.OPT_OVERLAP)}
-        for name, relay, overlap in (("direct", 0, 1), ("direct_serial", 0, 0)):
+        defaults = {o: comm.get_option(o) for o in (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE)}
+        # direct: one pull kernel per step; direct_serial: plus the step-0 copy inline;
+        # copy_engine: hipMemcpyAsync of the partner's window + a local reduce kernel
+        for name, relay, overlap, ce in (("direct", 0, 1, 0), ("direct_serial", 0, 0, 0), ("copy_engine", 0, 1, 1)):
             comm.set_option(ftar.OPT_RELAY, relay)
             comm.set_option(ftar.OPT_OVERLAP, overlap)
+            comm.set_option(ftar.OPT_COPY_ENGINE, ce)
             tv, _ = timed(raben)
-            tv_rd, _ = timed(rd) if name == "direct" else (None, None)
+            tv_rd, _ = timed(rd) if name in ("direct", "copy_engine") else (None, None)
             transports[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2)}
             if tv_rd:
                 transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})

@@ -73,6 +73,9 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
 /* Enqueue on the rank's background stream, ordered after everything queued so far on
  * the main stream (it then overlaps later main-stream work). */
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+/* Runtime copy (hipMemcpyAsync: SDMA / blit engine) of `bytes` on the main (bg = 0) or
+ * background (bg = 1) stream; `remote` = the source is a peer mapping. */
+int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int remote, int tag);
 /* Spin until the background stream drained. */
 int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg);
 /* Make the rank's stream wait for everything queued on `user_stream` (hipStream_t). */

@@ -254,6 +254,39 @@ int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, 
     return run_on(d, d->bg, dtype, op, segs, nseg, tag);
 }
 
+int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int remote, int tag)
+{
+    if (tag < 0 || tag >= FDEV_NTAGS) return 13;
+    if (bytes == 0) return 0;
+    hipStream_t st = d->stream;
+    if (bg) { // ordered after the main stream, like fdev_run_bg
+        hipEvent_t e = get_event(d);
+        if (!e) return set_err(hipErrorOutOfMemory, "hipEventCreate");
+        HIPCHK(hipEventRecord(e, d->stream));
+        HIPCHK(hipStreamWaitEvent(d->bg, e, 0));
+        d->event_pool.push_back(e);
+        st = d->bg;
+    }
+    if (remote) {
+        d->ctr.link_bytes += (double)bytes;
+        d->ctr.hbm_bytes += (double)bytes; // the local write
+    } else {
+        d->ctr.hbm_bytes += 2.0 * (double)bytes;
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (d->profiling) {
+        e0 = get_event(d);
+        e1 = get_event(d);
+        if (e0) (void)hipEventRecord(e0, st);
+    }
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+    if (d->profiling && e0 && e1) {
+        (void)hipEventRecord(e1, st);
+        d->pending.push_back(Pending{e0, e1, tag});
+    }
+    return 0;
+}
+
 int fdev_order_after(ftar_dev *d, void *user_stream)
 {
     hipEvent_t e = get_event(d);

@@ -54,6 +54,7 @@ struct ftar_comm {
     int overlap;         /* FTAR_OVERLAP (default 1): Raben step-0 redundancy copy on the background stream */
     int relay;           /* FTAR_RELAY (default 1): stripe exchanges over 2-hop paths */
     size_t relay_min;    /* FTAR_RELAY_MIN bytes: smallest per-rank window that is relayed */
+    int copy_engine;     /* FTAR_COPY_ENGINE (default 0): direct pulls by hipMemcpyAsync */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
 };
 
@@ -123,6 +124,9 @@ typedef struct {
 void ftar_plan_clear(ftar_plan *p);
 /* phase 1 (+ mid barrier + phase 2 when relayed); `skip` = this rank's source is dead;
  * (kphase, kstep) place the FTAR_PT_AFTER injection point after phase 1 */
+/* Launch a direct step's pull segments: one segment kernel, or with copy_engine the
+ * runtime copy engine for every remote operand (reduces staged through R). */
+void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int bg);
 void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag, int skip, int kphase, int kstep,
                     ftar_xstate *st);
 /* after the step's agree returned `known`: re-pull stripes lost with relays that died

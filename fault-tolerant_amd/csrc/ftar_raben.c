@@ -326,8 +326,8 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                                at(x, PIN, pl[0].off), (size_t)pl[0].n};
                 fdev_seg s1 = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
                                (size_t)pl[1].n};
-                ftar_run(c, x->dtype, x->op, &s0, 1, FDEV_TAG_STEP0);
-                ftar_run_bg(c, x->dtype, x->op, &s1, 1, FDEV_TAG_BG);
+                ftar_run_pulls(c, x->dtype, x->op, &s0, 1, FDEV_TAG_STEP0, 0);
+                ftar_run_pulls(c, x->dtype, x->op, &s1, 1, FDEV_TAG_BG, 1);
                 x->bg_pending = 1;
                 ftar_drain(c);
             }

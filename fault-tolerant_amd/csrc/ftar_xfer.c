@@ -27,6 +27,7 @@
  */
 #include "ftar_internal.h"
 
+#include <stdio.h>
 #include <string.h>
 
 #define STRIPE_ALIGN 256 /* elements; interior stripe boundaries are multiples of this */
@@ -133,6 +134,60 @@ static fdev_seg own_seg(ftar_comm *c, const ftar_pull *pl, int64_t st, int64_t l
     return s;
 }
 
+/* staging slot in R for a segment whose output lies in IN, W or T (same offset) */
+static void *staging_of(ftar_comm *c, const void *out)
+{
+    const char *o = (const char *)out;
+    for (int b = WS_IN; b <= WS_T; b++) {
+        const char *base = (const char *)c->ws[b];
+        if (base && o >= base && o < base + c->ws_bytes) return (char *)c->ws[WS_R] + (o - base);
+    }
+    return NULL;
+}
+
+void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int bg)
+{
+    if (!c->copy_engine) {
+        if (bg) ftar_run_bg(c, dtype, op, segs, nseg, tag);
+        else ftar_run(c, dtype, op, segs, nseg, tag);
+        return;
+    }
+    /* The reference's shape: the exchange is a copy (hipMemcpyAsync over xGMI, SDMA or
+     * blit engine) and the reduce a separate local kernel over the received window. */
+    size_t es = ftar_esize(dtype);
+    fdev_seg local[FDEV_MAX_SEGS];
+    int nl = 0;
+    for (int i = 0; i < nseg; i++) {
+        fdev_seg t = segs[i];
+        int rc = 0;
+        if (!t.remote) {
+            local[nl++] = t;
+        } else if (t.kind == FDEV_COPY) {
+            rc = fdev_copy(c->dev, bg, t.out, t.x, t.n * es, 1, tag);
+        } else {
+            void *stage = staging_of(c, t.out);
+            if (!stage) {
+                local[nl++] = t;
+                continue;
+            }
+            const void *src = (t.remote & FDEV_REMOTE_X) ? t.x : t.y;
+            rc = fdev_copy(c->dev, bg, stage, src, t.n * es, 1, tag);
+            if (t.remote & FDEV_REMOTE_X) t.x = stage;
+            else t.y = stage;
+            t.remote = 0;
+            local[nl++] = t;
+        }
+        if (rc) {
+            fprintf(stderr, "ftar: rank %d: copy failed: %s\n", c->wrank, fdev_last_error());
+            ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+        }
+    }
+    if (nl) {
+        if (bg) ftar_run_bg(c, dtype, op, local, nl, tag);
+        else ftar_run(c, dtype, op, local, nl, tag);
+    }
+}
+
 void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag, int skip, int kphase, int kstep,
                     ftar_xstate *xs)
 {
@@ -149,7 +204,7 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
                 segs[ns++] = own_seg(c, pl, pl->off, pl->n, at(ftar_buf(c, pl->src, pl->src_buf), pl->off, es), es);
             }
         if (ns) {
-            ftar_run(c, dtype, op, segs, ns, tag);
+            ftar_run_pulls(c, dtype, op, segs, ns, tag, 0);
             ftar_drain(c);
         }
         ftar_maybe_die(c, kphase, kstep, FTAR_PT_AFTER);

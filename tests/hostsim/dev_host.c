@@ -180,6 +180,14 @@ int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, 
 
 int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg) { return poll ? poll(arg) : 0; }
 
+int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int remote, int tag)
+{
+    memmove(dst, src, bytes);
+    if (remote) d->ctr.link_bytes += (double)bytes;
+    d->ctr.launches[tag]++;
+    return 0;
+}
+
 int fdev_order_after(ftar_dev *d, void *s) { return 0; }
 
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)

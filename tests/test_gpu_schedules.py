@@ -146,3 +146,21 @@ def test_large_windows_interleaved(oracle, algo, p, relay):
                   env=RELAY_ALL if relay else {"FTAR_RELAY": "0"})
     if relay:
         assert min(st[0][8] for st in r.status.values()) > 0
+
+
+CE = {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"}
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [2, 5, 8])
+def test_copy_engine_nofault(oracle, algo, p):
+    """Direct pulls by hipMemcpyAsync (copy engine) + local reduce kernels."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    _check(fn, algo, oracle.random_inputs(p, 100003, seed=p + 50), env=CE)
+
+
+@pytest.mark.parametrize("algo,kill", [("raben", (5, 1, 1, 2)), ("rd", (3, 1, 1, 2))])
+def test_copy_engine_kill(oracle, algo, kill):
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    p = 9 if algo == "raben" else 8
+    _check(fn, algo, oracle.random_inputs(p, 65536 + 9, seed=60), [kill], env=CE)

@@ -217,3 +217,30 @@ def test_relay_multi_kill_random(hostsim, oracle, seed):
     victims = rng.sample(range(p), rng.choice([1, 2]))
     kills = [(v, rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(3), rng.randrange(3)) for v in victims]
     _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 2049, seed=seed), kills, env=RELAY_ALL)
+
+
+CE = {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"}
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [2, 3, 4, 5, 8, 9])
+def test_copy_engine_nofault_parity(hostsim, oracle, algo, p):
+    """Direct pulls as runtime copies + a local reduce over the staged window."""
+    _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 4099, seed=p + 7), env=CE)
+
+
+@pytest.mark.parametrize("algo,p", [("raben", 9), ("rd", 8), ("rd", 6)])
+def test_copy_engine_single_kill_sweep(hostsim, oracle, algo, p):
+    ins = oracle.random_inputs(p, 1031, seed=p + 3)
+    fn = _fn(oracle, algo)
+    phases = [1, 2] if algo == "raben" else [1]
+    n = 0
+    for v in range(p):
+        for ph in phases:
+            for st in range(3):
+                ks = [(v, ph, st, 2)]
+                if fn(ins, ks).status[v] != oracle.DEAD:
+                    continue
+                _cmp(fn, algo, ins, ks, env=CE)
+                n += 1
+    assert n > 0
