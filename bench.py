@@ -216,13 +216,18 @@ def multi(args):
     # without the background-stream redundancy copy -- the reference's transport shape
     transports = {}
     if not args.no_variants:
-        defaults = {o: comm.get_option(o) for o in (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE)}
+        opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY)
+        defaults = {o: comm.get_option(o) for o in opts}
         # direct: one pull kernel per step; direct_serial: plus the step-0 copy inline;
-        # copy_engine: hipMemcpyAsync of the partner's window + a local reduce kernel
-        for name, relay, overlap, ce in (("direct", 0, 1, 0), ("direct_serial", 0, 0, 0), ("copy_engine", 0, 1, 1)):
-            comm.set_option(ftar.OPT_RELAY, relay)
-            comm.set_option(ftar.OPT_OVERLAP, overlap)
-            comm.set_option(ftar.OPT_COPY_ENGINE, ce)
+        # copy_engine: hipMemcpyAsync of the partner's window + a local reduce kernel;
+        # reference_shape: pairwise, inline, with the step-0 full exchange even where no
+        # handler can use it (the reference's data movement); relay_full_exchange: the
+        # default transport with that full exchange
+        variants = (("direct", (0, 1, 0, 0)), ("direct_serial", (0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0)),
+                    ("reference_shape", (0, 0, 0, 1)), ("relay_full_exchange", (1, 1, 0, 1)))
+        for name, vals in variants:
+            for o, v in zip(opts, vals):
+                comm.set_option(o, v)
             tv, _ = timed(raben)
             tv_rd, _ = timed(rd) if name in ("direct", "copy_engine") else (None, None)
             transports[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2)}
@@ -252,18 +257,23 @@ def multi(args):
         t_nc, _ = timed(rccl)
     L = world.bit_length() - 1
     r = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
-    # Link bytes per rank per direction on the critical path: the FT
-    # step-0 full exchange makes the schedule move (2.5 - 2^(1-L)) S; with the redundancy
-    # half on the background stream the critical path of a direct transport carries
-    # 2 (1 - 2^-L) S on one link per step.  A relayed step moves 2/(r-1) of its window
-    # per link (two phases over r-1 links).
+    # Link bytes per rank per direction.  The reference's FT Raben moves
+    # (2.5 - 2^(1-L)) S: its step 0 exchanges the full vector, half of it only as
+    # recovery data.  At power-of-two p no handler can use that half (they all abort
+    # without a spare), so the build skips it there and moves classic Rabenseifner's
+    # 2 (1 - 2^-L) S.  A relayed step moves 2/(r-1) of its window per link (two phases
+    # over r-1 links); a direct step moves it over one link.
     ft_bytes = (2.5 - 2.0 ** (1 - L)) * S
+    classic = 2 * (1 - 2.0 ** -L) * S
+    keep = world != r or comm.get_option(ftar.OPT_REDUNDANCY) != 0
+    sched_bytes = ft_bytes if keep else classic
     if relayed:
-        t_roof = 2.0 / (r - 1) * ft_bytes / (XGMI_LINK_GBS * 1e9)
-    elif os.environ.get("FTAR_OVERLAP", "1") != "0":
-        t_roof = 2 * (1 - 2.0 ** -L) * S / (XGMI_LINK_GBS * 1e9)
+        t_roof = 2.0 / (r - 1) * sched_bytes / (XGMI_LINK_GBS * 1e9)
+    elif comm.get_option(ftar.OPT_OVERLAP) != 0:
+        t_roof = classic / (XGMI_LINK_GBS * 1e9)
     else:
-        t_roof = ft_bytes / (XGMI_LINK_GBS * 1e9)
+        t_roof = sched_bytes / (XGMI_LINK_GBS * 1e9)
+    t_survey = ft_bytes / (XGMI_LINK_GBS * 1e9)  # the FT schedule on one link per step
     links = (r - 1) if relayed else 1
     peak = links * XGMI_LINK_GBS
     achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernels' pulled bytes
@@ -278,9 +288,11 @@ def multi(args):
                        "count": args.count, "parallelism": f"{world} ranks"},
             "algbw_GBps": round(S / t_rb / 1e9, 2),
             "transport": "relay2hop" if relayed else "direct",
-            "schedule_link_roofline": {"ft_schedule_bytes_per_rank": ft_bytes, "link_GBps": XGMI_LINK_GBS,
+            "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "link_GBps": XGMI_LINK_GBS,
                                        "links_per_step": links, "t_roof_ms": round(t_roof * 1e3, 3),
-                                       "frac": round(t_roof / t_rb, 4)},
+                                       "frac": round(t_roof / t_rb, 4),
+                                       "survey_ft_roofline_ms": round(t_survey * 1e3, 3),
+                                       "frac_of_survey_roofline": round(t_survey / t_rb, 4)},
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
                          "peak": peak, "unit": "GB/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,

@@ -126,6 +126,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->loop_seconds = getenv("FTAR_LOOP_SECONDS") ? atof(getenv("FTAR_LOOP_SECONDS")) : 0.0;
     c->overlap = getenv("FTAR_OVERLAP") ? atoi(getenv("FTAR_OVERLAP")) : 1;
     c->relay = getenv("FTAR_RELAY") ? atoi(getenv("FTAR_RELAY")) : 1;
+    c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 0;
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)4 << 20);
     int create = getenv("FTAR_LAUNCHER") == NULL;
@@ -266,6 +267,7 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_RELAY_MIN: c->relay_min = (size_t)v; break;
     case FTAR_OPT_LOOP_SECONDS: c->loop_seconds = v; break;
     case FTAR_OPT_COPY_ENGINE: c->copy_engine = v != 0; break;
+    case FTAR_OPT_REDUNDANCY: c->redundancy = v != 0; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;
@@ -280,6 +282,7 @@ int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
     case FTAR_OPT_RELAY_MIN: *v = (double)c->relay_min; break;
     case FTAR_OPT_LOOP_SECONDS: *v = c->loop_seconds; break;
     case FTAR_OPT_COPY_ENGINE: *v = c->copy_engine; break;
+    case FTAR_OPT_REDUNDANCY: *v = c->redundancy; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;

@@ -55,6 +55,7 @@ struct ftar_comm {
     int relay;           /* FTAR_RELAY (default 1): stripe exchanges over 2-hop paths */
     size_t relay_min;    /* FTAR_RELAY_MIN bytes: smallest per-rank window that is relayed */
     int copy_engine;     /* FTAR_COPY_ENGINE (default 0): direct pulls by hipMemcpyAsync */
+    int redundancy;      /* FTAR_REDUNDANCY (default 0 = only when a spare can use it) */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
 };
 

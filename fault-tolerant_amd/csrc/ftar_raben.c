@@ -38,6 +38,7 @@ typedef struct {
     size_t es, count;
     int steps, adjsize, rem;
     int rank, vrank, corr, has_recov;
+    int keep_recov; /* step 0 also pulls the partner's other half into T (recovery data) */
     int bg_pending; /* step-0 redundancy copy still running on the background stream */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
 } rb_ctx;
@@ -107,7 +108,7 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
         } else if (step == 0) {
             pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, WS_IN, ri[0], rc[0]};
             pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0]};
-            P->npull[cr] = 2;
+            P->npull[cr] = x->keep_recov ? 2 : 1;
         } else {
             pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_W, WS_W, WS_W, ri[step], rc[step]};
             P->npull[cr] = 1;
@@ -259,7 +260,13 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     if (count > (size_t)INT64_MAX / 16 || !sbuf || !rbuf) return FTAR_ERR_ARG;
     x->adjsize = 1 << x->steps;
     x->rem = c->size - x->adjsize;
-    x->has_recov = 1;
+    /* The step-0 copy of the partner's other half (tmp, :191-197) is only ever read by
+     * an RS error handler's replay, and every handler aborts before replaying when
+     * there is no idle spare (new_entry = 2 rem - 1 = -1, errhandler.c:207-211,377-378).
+     * rem only decreases during a call, so with rem = 0 at the start the copy can never
+     * be consumed: skip it (FTAR_REDUNDANCY=1 keeps it, the reference's shape). */
+    x->keep_recov = c->redundancy || x->rem > 0;
+    x->has_recov = x->keep_recov;
     ftar_stats_begin(c);
 
     size_t bytes = count * x->es;
@@ -327,8 +334,10 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                 fdev_seg s1 = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
                                (size_t)pl[1].n};
                 ftar_run_pulls(c, x->dtype, x->op, &s0, 1, FDEV_TAG_STEP0, 0);
-                ftar_run_pulls(c, x->dtype, x->op, &s1, 1, FDEV_TAG_BG, 1);
-                x->bg_pending = 1;
+                if (x->keep_recov) {
+                    ftar_run_pulls(c, x->dtype, x->op, &s1, 1, FDEV_TAG_BG, 1);
+                    x->bg_pending = 1;
+                }
                 ftar_drain(c);
             }
             ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_AFTER);

@@ -160,7 +160,8 @@ typedef enum {
     FTAR_OPT_RELAY = 1,        /* stripe exchanges over 2-hop relay paths (0/1) */
     FTAR_OPT_RELAY_MIN = 2,    /* smallest window, in bytes, that is relayed */
     FTAR_OPT_LOOP_SECONDS = 3, /* stretch of the step loop for fault-injection runs */
-    FTAR_OPT_COPY_ENGINE = 4   /* direct pulls as hipMemcpyAsync copies + local reduce (0/1) */
+    FTAR_OPT_COPY_ENGINE = 4,  /* direct pulls as hipMemcpyAsync copies + local reduce (0/1) */
+    FTAR_OPT_REDUNDANCY = 5    /* Raben step-0 recovery copy: 0 only when a spare exists, 1 always */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);

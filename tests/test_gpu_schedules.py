@@ -164,3 +164,10 @@ def test_copy_engine_kill(oracle, algo, kill):
     fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
     p = 9 if algo == "raben" else 8
     _check(fn, algo, oracle.random_inputs(p, 65536 + 9, seed=60), [kill], env=CE)
+
+
+@pytest.mark.parametrize("p,kill", [(8, None), (4, None), (8, (3, 1, 1, 2)), (8, (5, 2, 1, 2))])
+def test_raben_redundancy_always(oracle, p, kill):
+    """The reference's step-0 full exchange kept at power-of-two p (FTAR_REDUNDANCY=1)."""
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(p, 100003, seed=p + 70),
+           [kill] if kill else [], env={"FTAR_REDUNDANCY": "1"})

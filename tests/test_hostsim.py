@@ -244,3 +244,17 @@ def test_copy_engine_single_kill_sweep(hostsim, oracle, algo, p):
                 _cmp(fn, algo, ins, ks, env=CE)
                 n += 1
     assert n > 0
+
+
+@pytest.mark.parametrize("p", [2, 4, 8])
+def test_raben_redundancy_always_pow2(hostsim, oracle, p):
+    """FTAR_REDUNDANCY=1 keeps the reference's step-0 full exchange at power-of-two p,
+    where the build skips the half no handler can use: same results and outcomes."""
+    ins = oracle.random_inputs(p, 2053, seed=p + 11)
+    env = {"FTAR_REDUNDANCY": "1"}
+    _cmp(oracle.rabenseifner, "raben", ins, env=env)
+    for v in range(p):
+        for ph, st in ((1, 0), (1, 1), (2, 0)):
+            ks = [(v, ph, st, 2)]
+            if oracle.rabenseifner(ins, ks).status[v] == oracle.DEAD:
+                _cmp(oracle.rabenseifner, "raben", ins, ks, env=env)
