@@ -192,6 +192,27 @@ def multi(args):
         rc = comm.recursive_doubling(x, y)
         assert rc == 0, rc
 
+    def quick(fn, steps=3, warmup=1):
+        saved = (args.steps, args.warmup)
+        args.steps, args.warmup = steps, warmup
+        try:
+            return timed(fn)[0]
+        finally:
+            args.steps, args.warmup = saved
+
+    # Transport selection before the timed run: the relay transport's gain depends on
+    # how the node's xGMI links behave under concurrent peer reads, so a short
+    # comparison (max over ranks, identical on every rank) picks relay or direct.
+    selection = None
+    if world >= 3 and not args.no_variants and comm.get_option(ftar.OPT_RELAY):
+        t_relay = quick(raben)
+        comm.set_option(ftar.OPT_RELAY, 0)
+        t_direct = quick(raben)
+        chosen = "relay2hop" if t_relay <= t_direct else "direct"
+        comm.set_option(ftar.OPT_RELAY, 1 if chosen == "relay2hop" else 0)
+        selection = {"relay2hop_ms": round(t_relay * 1e3, 4), "direct_ms": round(t_direct * 1e3, 4),
+                     "chosen": chosen}
+
     t_rb, k_rb = timed(raben)
     step0_bytes = timed.link_bytes
     relayed = comm.last_stats().relayed_steps > 0
@@ -304,6 +325,7 @@ def multi(args):
                    "step0_kernel_ms": round(k_rd, 4)},
             "rccl_allreduce": ({"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2)}
                                if t_nc else None),
+            "transport_selection": selection,
             "transports": transports,
             "max_abs_err_vs_rccl": err,
             "int32_rank_checksum_ok": {"raben": cks_raben == cks_want, "rd": cks_rd == cks_want},

@@ -195,8 +195,10 @@ static hipEvent_t get_event(ftar_dev *d)
         d->event_pool.pop_back();
         return e;
     }
+    // pooled events only time kernels and order streams of this device: no system fence
+    // (the cross-GPU visibility fence is sync_stream's dedicated marker)
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     return e;
 }
 
