@@ -54,3 +54,14 @@ def test_single_kill_is_classified(hostsim, tmp_path, algo):
     assert r["RIGHT RESULT"] == "True"
     assert (r["KILLED"] == "1" and r["ABORT"] == "False") or (r["ABORT"] == "True" and int(r["KILLED"]) == n) \
         or r["KILLED"] == "0", r
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+def test_multiple_kill_is_classified(hostsim, tmp_path, algo):
+    """KILL=2 (run_mpi.sh picks 1..N-1 victims, killed 0.5 s apart): a recovery with the
+    right result, or a clean MPI_Abort -- never a deadlock, a crash or a wrong result."""
+    cp, rows = _run_test(tmp_path, 2, algo)
+    assert len(rows) == 1, cp.stdout + cp.stderr
+    r = rows[0]
+    assert r["DEADLOCK"] == "False" and r["SEGFAULT"] == "False", (r, cp.stdout + cp.stderr)
+    assert r["RIGHT RESULT"] == "True", r
