@@ -153,7 +153,8 @@ def multi(args):
     local = int(os.environ.get("LOCAL_RANK", rank))
     # FTAR_DEVICE pins every rank to one GPU (single-GPU rehearsal of the multi-rank path;
     # RCCL refuses two ranks on one device, so such runs use --dist-backend gloo)
-    dev = int(os.environ.get("FTAR_DEVICE", local))
+    dev = int(os.environ.get("FTAR_DEVICE", local)) % max(1, torch.cuda.device_count())
+    os.environ.setdefault("FTAR_DEVICE", str(dev))  # the library opens the same device
     torch.cuda.set_device(dev)
     dist.init_process_group(backend=args.dist_backend)
     comm = ftar.Comm.from_env()
