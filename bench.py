@@ -283,14 +283,14 @@ def multi(args):
     # (2.5 - 2^(1-L)) S: its step 0 exchanges the full vector, half of it only as
     # recovery data.  At power-of-two p no handler can use that half (they all abort
     # without a spare), so the build skips it there and moves classic Rabenseifner's
-    # 2 (1 - 2^-L) S.  A relayed step moves 2/(r-1) of its window per link (two phases
+    # 2 (1 - 2^-L) S.  A relayed step moves 2/r of its window per link (two phases
     # over r-1 links); a direct step moves it over one link.
     ft_bytes = (2.5 - 2.0 ** (1 - L)) * S
     classic = 2 * (1 - 2.0 ** -L) * S
     keep = world != r or comm.get_option(ftar.OPT_REDUNDANCY) != 0
     sched_bytes = ft_bytes if keep else classic
     if relayed:
-        t_roof = 2.0 / (r - 1) * sched_bytes / (XGMI_LINK_GBS * 1e9)
+        t_roof = 2.0 / r * sched_bytes / (XGMI_LINK_GBS * 1e9)
     elif comm.get_option(ftar.OPT_OVERLAP) != 0:
         t_roof = classic / (XGMI_LINK_GBS * 1e9)
     else:

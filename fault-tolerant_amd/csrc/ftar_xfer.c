@@ -11,11 +11,13 @@
  *            (X being Y's j-th relay) out of Y's partner's HBM into X's relay buffer R;
  *   barrier  (agree round: a relay that died before it is known to every rank);
  *   phase 2  Y pulls its relayed stripes from the relays' R buffers and reduces (or
- *            copies) them into its window.
+ *            copies) them into its window, and its last stripe directly from its
+ *            partner (that link is otherwise idle in phase 2).
  *
- * With r receivers every link of a rank carries 1/(r-1) of a window per phase instead
- * of the whole window on one link: for r = 8 a step costs about 2/7 of the direct
- * exchange.  Results are bit-identical to the direct pull: every element is still
+ * A window is cut into r stripes (r receivers): two direct ones (one per phase) and
+ * r - 2 relayed ones.  Every link of a rank then carries 1/r of a window per phase
+ * instead of the whole window on one link: for r = 8 a step costs about 2/8 of the
+ * direct exchange.  Results are bit-identical to the direct pull: every element is still
  * combined once, with the same operands in the same roles.
  *
  * Faults: the pulled data is always the partner's window, stable since the previous
@@ -54,6 +56,10 @@ static int relays_of(const ftar_comm *c, const ftar_plan *p, const int *R, int n
     return k;
 }
 
+/* stripes of a window with k relays: 0 = direct in phase 1, 1..k relayed (relay j-1),
+ * k + 1 = direct in phase 2 */
+static int nstripes(int k) { return k + 2; }
+
 static void stripe(const ftar_pull *pl, int nst, int j, int64_t *start, int64_t *len)
 {
     int64_t base = (pl->n / nst) / STRIPE_ALIGN * STRIPE_ALIGN;
@@ -80,7 +86,7 @@ static int64_t slot_of(const ftar_comm *c, const ftar_plan *p, const int *R, int
         if (idx < 0) continue;
         for (int uu = 0; uu < p->npull[yy]; uu++) {
             int64_t st, len;
-            stripe(&p->pull[yy][uu], k + 1, idx + 1, &st, &len);
+            stripe(&p->pull[yy][uu], nstripes(k), idx + 1, &st, &len);
             int64_t slot = round_up(off, SLOT_PAD) + (st % SLOT_PAD);
             if (yy == y && uu == u) found = slot;
             off = slot + len;
@@ -220,7 +226,7 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
         for (int u = 0; u < p->npull[me]; u++) {
             const ftar_pull *pl = &p->pull[me][u];
             int64_t st, len;
-            stripe(pl, k + 1, 0, &st, &len);
+            stripe(pl, nstripes(k), 0, &st, &len);
             if (len > 0) segs[ns++] = own_seg(c, pl, st, len, at(ftar_buf(c, pl->src, pl->src_buf), st, es), es);
         }
     }
@@ -235,7 +241,7 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
         for (int u = 0; u < p->npull[y]; u++) {
             const ftar_pull *pl = &p->pull[y][u];
             int64_t st, len;
-            stripe(pl, k + 1, idx + 1, &st, &len);
+            stripe(pl, nstripes(k), idx + 1, &st, &len);
             if (len <= 0) continue;
             int64_t slot = slot_of(c, p, R, nr, me, y, u, NULL);
             fdev_seg s;
@@ -263,7 +269,7 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
             const ftar_pull *pl = &p->pull[me][u];
             for (int t = 0; t < k; t++) {
                 int64_t st, len;
-                stripe(pl, k + 1, t + 1, &st, &len);
+                stripe(pl, nstripes(k), t + 1, &st, &len);
                 if (len <= 0) continue;
                 int xw = c->order[rel[t]];
                 if (xs->mid_dead & (1ull << xw)) {
@@ -273,6 +279,9 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
                 int64_t slot = slot_of(c, p, R, nr, rel[t], me, u, NULL);
                 segs[ns++] = own_seg(c, pl, st, len, at(ftar_buf(c, xw, WS_R), slot, es), es);
             }
+            int64_t st, len; /* the phase-2 direct stripe (the partner's window is stable) */
+            stripe(pl, nstripes(k), k + 1, &st, &len);
+            if (len > 0) segs[ns++] = own_seg(c, pl, st, len, at(ftar_buf(c, pl->src, pl->src_buf), st, es), es);
         }
     }
     if (ns) {
@@ -297,7 +306,7 @@ void ftar_xfer_repair(ftar_comm *c, const ftar_plan *p, int dtype, int op, ftar_
             for (int t = 0; t < k; t++) {
                 if (!(xs->mid_dead & (1ull << c->order[rel[t]]))) continue;
                 int64_t st, len;
-                stripe(pl, k + 1, t + 1, &st, &len);
+                stripe(pl, nstripes(k), t + 1, &st, &len);
                 if (len > 0)
                     segs[ns++] = own_seg(c, pl, st, len, at(ftar_buf(c, pl->src, pl->src_buf), st, es), es);
             }

@@ -99,6 +99,26 @@ __global__ void k_lds(float4 *__restrict__ io, const float4 *__restrict__ in, si
     }
 }
 
+// one tile of U*BS vectors per block (the product's mapping); XCD = 1 remaps blocks so
+// each XCD (blocks round-robin over 8 XCDs) streams one contiguous eighth of the data
+template <int U, int BS, int XCD>
+__global__ __launch_bounds__(BS) void k_tile(float4 *__restrict__ io, const float4 *__restrict__ in, size_t nv)
+{
+    unsigned b = blockIdx.x;
+    if constexpr (XCD) {
+        const unsigned per = gridDim.x / 8;
+        b = (b % 8) * per + b / 8;
+    }
+    const size_t base = (size_t)b * U * BS + threadIdx.x;
+    float4 a[U], c[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) a[u] = ld<true>(io + base + u * BS);
+#pragma unroll
+    for (int u = 0; u < U; u++) c[u] = ld<true>(in + base + u * BS);
+#pragma unroll
+    for (int u = 0; u < U; u++) io[base + u * BS] = add4(a[u], c[u]);
+}
+
 __global__ void k_fill(float4 *p, size_t nv, float s)
 {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (size_t)gridDim.x * blockDim.x)
@@ -155,6 +175,23 @@ int main(int argc, char **argv)
     snprintf(nm, sizeof(nm), "bc U%d ntl%d nts%d bs%d grid%d", U, NTL, NTS, BS, G);                        \
     run(nm, [&] { size_t ch = (nv + G - 1) / G; k_bc<U, NTL, NTS><<<G, BS>>>(io, in, nv, ch); });
 
+    if (argc > 2 && argv[2][0] == 't') { // tile mapping variants (nv divisible by every tile)
+#define TL(U, BS, X)                                                                                        \
+    snprintf(nm, sizeof(nm), "tile U%d bs%d xcd%d", U, BS, X);                                             \
+    run(nm, [&] { k_tile<U, BS, X><<<(unsigned)(nv / (U * BS)), BS>>>(io, in, nv); });
+        TL(2, 256, 0)
+        TL(2, 256, 1)
+        TL(1, 256, 0)
+        TL(4, 256, 0)
+        TL(4, 256, 1)
+        TL(2, 128, 0)
+        TL(4, 128, 0)
+        TL(2, 512, 0)
+        TL(1, 512, 0)
+        TL(8, 256, 0)
+        TL(2, 256, 0)
+        goto done;
+    }
     if (argc > 2) { // focused sweep around the optimum
         for (int G : {4096, 8192, 16384, 32768}) {
             GS(4, 1, 0, 256, G)
