@@ -1,0 +1,48 @@
+"""Transport options of the C ABI (ftar_comm_set_option / get_option), exercised through
+the host-sim build of the same C sources (a one-rank comm needs no GPU)."""
+import ctypes
+import os
+
+import pytest
+
+
+@pytest.fixture
+def solo(hostsim, monkeypatch):
+    for k in ("FTAR_RELAY", "FTAR_RELAY_MIN", "FTAR_OVERLAP", "FTAR_COPY_ENGINE", "FTAR_REDUNDANCY"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("FTAR_HOSTSIM_TAG", f"opt{os.getpid()}")
+    L = ctypes.CDLL(os.path.join(hostsim, "libftar_hostsim.so"))
+    L.ftar_init_rank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int]
+    L.ftar_comm_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+    L.ftar_comm_get_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    L.ftar_finalize.argtypes = [ctypes.c_void_p]
+    h = ctypes.c_void_p()
+    assert L.ftar_init_rank(ctypes.byref(h), f"/ftar-opt-{os.getpid()}".encode(), 0, 1, 0) == 0
+    yield L, h
+    L.ftar_finalize(h)
+
+
+def _get(L, h, opt):
+    v = ctypes.c_double()
+    assert L.ftar_comm_get_option(h, opt, ctypes.byref(v)) == 0
+    return v.value
+
+
+def test_option_defaults_and_roundtrip(solo):
+    L, h = solo
+    # defaults: overlap on, relay on (4 MiB threshold), loop stretch off, copy engine off,
+    # redundancy only where a spare can use it
+    assert [_get(L, h, o) for o in range(6)] == [1.0, 1.0, float(4 << 20), 0.0, 0.0, 0.0]
+    for opt, val in ((0, 0), (1, 0), (2, 1 << 20), (3, 0.5), (4, 1), (5, 1)):
+        assert L.ftar_comm_set_option(h, opt, val) == 0
+        assert _get(L, h, opt) == val
+
+
+def test_option_errors(solo):
+    L, h = solo
+    assert L.ftar_comm_set_option(h, 99, 1) == 13       # FTAR_ERR_ARG
+    assert L.ftar_comm_set_option(h, 2, -1) == 13
+    assert L.ftar_comm_set_option(None, 0, 1) == 13
+    v = ctypes.c_double()
+    assert L.ftar_comm_get_option(h, 99, ctypes.byref(v)) == 13
