@@ -258,3 +258,18 @@ def test_raben_redundancy_always_pow2(hostsim, oracle, p):
             ks = [(v, ph, st, 2)]
             if oracle.rabenseifner(ins, ks).status[v] == oracle.DEAD:
                 _cmp(oracle.rabenseifner, "raben", ins, ks, env=env)
+
+
+@pytest.mark.parametrize("algo,p", [("rd", 12), ("rd", 16), ("rd", 24), ("rd", 32), ("raben", 17), ("raben", 33),
+                                    ("raben", 60), ("raben", 64), ("rd", 64)])
+def test_campaign_sizes(hostsim, oracle, algo, p):
+    """The reference's fault-campaign N (data/data_fault: RD 4..32, Raben 5..60) and
+    the 64-rank maximum: no-fault parity plus single kills at seeded points."""
+    fn = _fn(oracle, algo)
+    ins = oracle.random_inputs(p, 1031, seed=p + 90)
+    _cmp(fn, algo, ins)
+    rng = random.Random(p)
+    steps = p.bit_length() - 1
+    for _ in range(3):
+        k = (rng.randrange(p), rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(steps), 2)
+        _cmp(fn, algo, ins, [k])
