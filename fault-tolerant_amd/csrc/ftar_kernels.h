@@ -40,6 +40,35 @@ struct KSegList {
     unsigned char il[kMaxIleave];
 };
 
+// What one workgroup of segment_kernel processes: piece `seg`, starting at tile (vector
+// pieces) or block slot (scalar pieces) `first`, then every `stride`-th one.  Shared by
+// the kernel and the host-side coverage test (tests/kernel_plan).
+struct BlockWork {
+    int seg;
+    size_t first;
+    size_t stride;
+};
+
+__host__ __device__ inline BlockWork map_block(const KSegList &L, unsigned b)
+{
+    BlockWork w;
+    if (b < L.il_blocks) { // interleaved prefix: chunk q of piece il[q % nil]
+        const unsigned q = b / kChunkTiles;
+        w.seg = L.il[q % (unsigned)L.nil];
+        w.first = (size_t)(q / (unsigned)L.nil) * kChunkTiles + b % kChunkTiles;
+        w.stride = L.s[w.seg].ntiles;
+        return w;
+    }
+    int si = 0;
+    while (si + 1 < L.nseg && b >= L.s[si].blk_end) si++;
+    const KSeg &S = L.s[si];
+    const size_t j = b - S.blk_begin, nblk = S.blk_end - S.blk_begin;
+    w.seg = si;
+    w.first = (S.vec ? S.tile_base : 0) + j;
+    w.stride = (S.vec && S.tile_base) ? S.ntiles : nblk;
+    return w;
+}
+
 struct SegIn {
     int kind;
     void *out;

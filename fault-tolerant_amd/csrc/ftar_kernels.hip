@@ -79,14 +79,6 @@ __device__ __forceinline__ uint4 ldnt(const uint4 *p)
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-__device__ __forceinline__ int find_segment(const KSegList &L, unsigned b)
-{
-    // blockIdx is wave-uniform; readfirstlane keeps the search in SGPRs.
-    int si = 0;
-    while (si + 1 < L.nseg && b >= L.s[si].blk_end) si++;
-    return __builtin_amdgcn_readfirstlane(si);
-}
-
 template <typename T, int OP>
 __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk)
 {
@@ -136,19 +128,12 @@ __device__ __forceinline__ void scalar_body(const KSeg &S, size_t b, size_t nblk
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void segment_kernel(KSegList L)
 {
+    // blockIdx is wave-uniform; readfirstlane keeps the lookup in SGPRs.
     const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
-    if (b < L.il_blocks) { // interleaved prefix: chunk q of piece il[q % nil]
-        const unsigned q = b / kChunkTiles;
-        const int si = __builtin_amdgcn_readfirstlane((int)L.il[q % (unsigned)L.nil]);
-        const KSeg &S = L.s[si];
-        vec_body<T, OP>(S, (size_t)(q / (unsigned)L.nil) * kChunkTiles + b % kChunkTiles, S.ntiles);
-        return;
-    }
-    const int si = find_segment(L, b);
-    const KSeg &S = L.s[si];
-    const size_t j = b - S.blk_begin;
-    if (S.vec) vec_body<T, OP>(S, S.tile_base + j, S.tile_base ? S.ntiles : S.blk_end - S.blk_begin);
-    else scalar_body<T, OP>(S, j, S.blk_end - S.blk_begin);
+    const BlockWork w = map_block(L, b);
+    const KSeg &S = L.s[__builtin_amdgcn_readfirstlane(w.seg)];
+    if (S.vec) vec_body<T, OP>(S, w.first, w.stride);
+    else scalar_body<T, OP>(S, w.first, w.stride);
 }
 
 // LDS-DMA staged local reduce (variant 1): the `in` operand is moved HBM -> LDS by
