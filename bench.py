@@ -85,16 +85,32 @@ def single(args):
     for _ in range(args.warmup):
         ftar.reduce_local(x, y)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for e0, e1 in evs:
+    if args.timing == "launch":
+        # an event pair around every launch: per-launch kernel time, at the cost of two
+        # timestamp markers between consecutive kernels in the timed region
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for e0, e1 in evs:
+            e0.record()
+            ftar.reduce_local(x, y)  # launched on torch's current stream, the one the events see
+            e1.record()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        k_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    else:
+        # one event pair around the whole timed region: the average launch duration
+        # includes the kernel-to-kernel boundaries, nothing is inserted between launches
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
         e0.record()
-        ftar.reduce_local(x, y)  # launched on torch's current stream, the one the events see
+        for _ in range(args.steps):
+            ftar.reduce_local(x, y)
         e1.record()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        k_ms = e0.elapsed_time(e1) / args.steps
     ms_step = (t1 - t0) * 1e3 / args.steps
-    k_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
     S = args.count * 4
     achieved = 3 * S / (k_ms * 1e-3) / 1e9
     out = {
@@ -102,7 +118,8 @@ def single(args):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic uniform[-1,1), HBM-resident",
         "config": {"workload": "configs[1]: local-reduce HIP kernel (MPI_Reduce_local), 2 x 256 MiB float32 SUM, "
-                               "1 MI355X", "count": args.count, "kernel_variant": args.variant},
+                               "1 MI355X", "count": args.count, "kernel_variant": args.variant,
+                   "timing": args.timing},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("reduce_local_c2"),
                      "kernel": "segment_kernel<float,SUM>", "algorithmic_bytes_per_launch": 3 * S,
@@ -345,6 +362,8 @@ def main():
     ap.add_argument("--count", type=int, default=COUNT)
     ap.add_argument("--variant", type=int, default=0, help="local-reduce kernel: 0 register, 1 LDS-DMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timing", choices=["region", "launch"], default="region",
+                    help="N=1 kernel time: events around the timed region, or around every launch")
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the direct-transport comparison")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for barrier/timing")
     args = ap.parse_args()
