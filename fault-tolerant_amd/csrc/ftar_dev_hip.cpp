@@ -66,7 +66,7 @@ struct ftar_dev {
     int device;
     hipStream_t stream;
     hipStream_t bg;
-    hipEvent_t fence_main; // system-scope release markers that sync_stream waits on
+    hipEvent_t fence_main; // fenced markers that sync_stream waits on
     hipEvent_t fence_bg;
     int profiling;
     unsigned max_blocks;
@@ -105,8 +105,10 @@ int fdev_open(int device, ftar_dev **out)
     if (d->max_blocks == 0) d->max_blocks = 2048;
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&d->bg, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&d->fence_main, hipEventDisableTiming | hipEventReleaseToSystem));
-    HIPCHK(hipEventCreateWithFlags(&d->fence_bg, hipEventDisableTiming | hipEventReleaseToSystem));
+    // default (fenced) events: recording one performs a system-scope sequentially
+    // consistent fence -- L2 writeback and invalidation -- see sync_stream
+    HIPCHK(hipEventCreateWithFlags(&d->fence_main, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d->fence_bg, hipEventDisableTiming));
     // Peer access to every other GPU of the node: the exchanges read peers' HBM.
     for (int p = 0; p < ndev; p++) {
         if (p == device) continue;
@@ -301,12 +303,14 @@ int fdev_order_after(ftar_dev *d, void *user_stream)
 
 static int harvest(ftar_dev *d);
 
-// Waits for everything enqueued on `st` by spinning on a system-scope release marker.
-// The marker is what makes a step's results visible to the peers that pull them next:
-// its release writes this GPU's dirty L2 lines back to HBM (peers read our HBM over
-// xGMI, not our L2) and its fence invalidates this GPU's cached copies of peer memory,
-// so the next step's pulls fetch the peers' new windows.  Without it the visibility of
-// a kernel's stores to other GPUs would depend on the runtime's default packet fences.
+// Waits for everything enqueued on `st` by spinning on a fenced marker event.  Its
+// system-scope sequentially consistent fence is what makes a step's results visible to
+// the peers that pull them next -- the writeback puts this GPU's dirty L2 lines in HBM
+// (peers read our HBM over xGMI, not our L2) -- and its invalidation drops this GPU's
+// cached copies of peer memory, so the next step's pulls (issued after the barrier,
+// with no peer reads in between) fetch the peers' new windows.  Without it the
+// visibility of a kernel's stores to other GPUs would rest on the runtime's default
+// packet fences.
 static int sync_stream(ftar_dev *d, hipStream_t st, int (*poll)(void *), void *arg)
 {
     hipEvent_t fence = st == d->bg ? d->fence_bg : d->fence_main;
