@@ -415,6 +415,13 @@ void ftar_shrink(ftar_comm *c, uint64_t failed)
 
 void *ftar_buf(ftar_comm *c, int w, int b) { return (w == c->wrank) ? c->ws[b] : c->peer[w][b]; }
 
+void *ftar_local(ftar_comm *c, int b)
+{
+    if (b == WS_UIN) return (void *)c->uin;
+    if (b == WS_UOUT) return c->uout;
+    return c->ws[b];
+}
+
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
 {
     if (bytes <= c->ws_bytes && c->ws[0]) return FTAR_SUCCESS;

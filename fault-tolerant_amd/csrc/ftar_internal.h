@@ -16,6 +16,10 @@
 #define WS_W 1   /* accumulator: Raben rbuf, RD ping-pong A */
 #define WS_T 2   /* Raben tmp (step-0 redundancy copy), RD ping-pong B */
 #define WS_R 3   /* relay staging: stripes this rank forwards for other ranks */
+/* the caller's buffers of the current call: never exported, so only the rank itself
+ * names them (a plan's x_buf / dst_buf, resolved by ftar_local) */
+#define WS_UIN 4  /* sbuf / src */
+#define WS_UOUT 5 /* rbuf / dst */
 
 
 struct ftar_comm {
@@ -42,6 +46,9 @@ struct ftar_comm {
     void *peer[FTAR_MAX_RANKS][FTAR_NBUF];
     size_t peer_bytes[FTAR_MAX_RANKS];
 
+    const void *uin; /* the current call's buffers (WS_UIN / WS_UOUT) */
+    void *uout;
+
     /* host staging for the _host entry points */
     void *hsend, *hrecv;
     size_t hbytes;
@@ -67,6 +74,8 @@ int ftar_comm_rank_of(const ftar_comm *c, int w);
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes);
 /* pointer to buffer b of original rank w (own or peer mapping) */
 void *ftar_buf(ftar_comm *c, int w, int b);
+/* this rank's buffer b: a workspace buffer or the call's WS_UIN / WS_UOUT */
+void *ftar_local(ftar_comm *c, int b);
 
 /* agree over the survivors; returns newly failed original ranks (not yet acked) */
 uint64_t ftar_sync(ftar_comm *c);
@@ -128,8 +137,10 @@ void ftar_plan_clear(ftar_plan *p);
 /* Launch a direct step's pull segments: one segment kernel, or with copy_engine the
  * runtime copy engine for every remote operand (reduces staged through R). */
 void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int bg);
+/* `extra` local segments (no peer reads) ride along in the step's first launch, even
+ * when this rank's pulls are skipped */
 void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag, int skip, int kphase, int kstep,
-                    ftar_xstate *st);
+                    const fdev_seg *extra, int nextra, ftar_xstate *st);
 /* after the step's agree returned `known`: re-pull stripes lost with relays that died
  * before the mid barrier, then one more (uniform) barrier */
 void ftar_xfer_repair(ftar_comm *c, const ftar_plan *p, int dtype, int op, ftar_xstate *st, uint64_t known);

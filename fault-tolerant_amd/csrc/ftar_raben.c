@@ -40,6 +40,7 @@ typedef struct {
     int rank, vrank, corr, has_recov;
     int keep_recov; /* step 0 also pulls the partner's other half into T (recovery data) */
     int bg_pending; /* step-0 redundancy copy still running on the background stream */
+    int fast_io;    /* power of two, no recovery data: sbuf/rbuf used in place (see below) */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
 } rb_ctx;
 
@@ -102,11 +103,12 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
         int src = c->order[rb_real(x, v ^ mask)];
         ftar_pull *pl = P->pull[cr];
         memset(pl, 0, sizeof(ftar_pull) * FTAR_MAX_PULLS);
-        if (ag) {
-            pl[0] = (ftar_pull){FDEV_COPY, 0, src, WS_W, WS_W, WS_W, si[step], sc[step]};
+        if (ag) { /* fast_io: the last allgather step lands in rbuf */
+            int dst = (x->fast_io && step == 0) ? WS_UOUT : WS_W;
+            pl[0] = (ftar_pull){FDEV_COPY, 0, src, WS_W, dst, WS_W, si[step], sc[step]};
             P->npull[cr] = 1;
-        } else if (step == 0) {
-            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, WS_IN, ri[0], rc[0]};
+        } else if (step == 0) { /* fast_io: the local operand is sbuf itself */
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, x->fast_io ? WS_UIN : WS_IN, ri[0], rc[0]};
             pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0]};
             P->npull[cr] = x->keep_recov ? 2 : 1;
         } else {
@@ -267,42 +269,62 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * be consumed: skip it (FTAR_REDUNDANCY=1 keeps it, the reference's shape). */
     x->keep_recov = c->redundancy || x->rem > 0;
     x->has_recov = x->keep_recov;
+    /* Without an idle rank every failure aborts (new_entry = -1, errhandler.c:207-211,
+     * 377-378), so nothing outside the schedule has to stay recoverable: step 0 reads
+     * this rank's reduce half straight from sbuf (only the half peers pull is staged in
+     * IN), the last allgather step writes rbuf directly and copies this rank's own final
+     * half out of W in the same launch, and the prologue's three barriers (no pre-step
+     * exchange at rem = 0) collapse into one.  Same operands, same bits. */
+    x->fast_io = !x->keep_recov && x->rem == 0 && x->steps >= 1;
+    c->uin = sbuf;
+    c->uout = rbuf;
     ftar_stats_begin(c);
 
     size_t bytes = count * x->es;
     ftar_ensure_workspace(c, bytes);
     void *IN = c->ws[WS_IN], *W = c->ws[WS_W], *T = c->ws[WS_T];
     fdev_order_after(c->dev, c->user_stream); /* sbuf may still be in flight on the caller's stream */
-    run_copy(x, IN, sbuf, (int64_t)count, 0, FDEV_TAG_LOCAL); /* rbuf = sbuf, :35-42 */
-    ftar_drain(c);
     rb_vrank(x);
+    if (x->fast_io) { /* the half of sbuf peers pull at step 0 */
+        rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+        run_copy(x, at(x, IN, x->sindex[0]), at(x, (void *)sbuf, x->sindex[0]), x->scount[0], 0, FDEV_TAG_LOCAL);
+    } else {
+        run_copy(x, IN, sbuf, (int64_t)count, 0, FDEV_TAG_LOCAL); /* rbuf = sbuf, :35-42 */
+    }
+    ftar_drain(c);
 
     /* ---- pre-step (:61-139): failures are fatal here ---- */
     ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BEFORE);
-    ftar_sync_fatal(c); /* every IN is ready */
-    int64_t lh = (int64_t)count / 2, rh = (int64_t)count - lh;
-    if (x->rank < 2 * x->rem) {
-        if (x->rank % 2 != 0) { /* odd: reduce the right half with the even's right half */
-            void *P = ftar_buf(c, c->order[x->rank - 1], WS_IN);
-            run_reduce(x, at(x, IN, lh), at(x, IN, lh), at(x, P, lh), rh, FDEV_REMOTE_Y, FDEV_TAG_STEP);
-        } else { /* even: reduce the left half with the odd's left half */
-            void *P = ftar_buf(c, c->order[x->rank + 1], WS_IN);
-            run_reduce(x, IN, IN, P, lh, FDEV_REMOTE_Y, FDEV_TAG_STEP);
+    if (x->fast_io) {
+        ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
+        ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
+        ftar_sync_fatal(c); /* every IN is ready; the barrier before the tolerant region (:166) */
+    } else {
+        ftar_sync_fatal(c); /* every IN is ready */
+        int64_t lh = (int64_t)count / 2, rh = (int64_t)count - lh;
+        if (x->rank < 2 * x->rem) {
+            if (x->rank % 2 != 0) { /* odd: reduce the right half with the even's right half */
+                void *P = ftar_buf(c, c->order[x->rank - 1], WS_IN);
+                run_reduce(x, at(x, IN, lh), at(x, IN, lh), at(x, P, lh), rh, FDEV_REMOTE_Y, FDEV_TAG_STEP);
+            } else { /* even: reduce the left half with the odd's left half */
+                void *P = ftar_buf(c, c->order[x->rank + 1], WS_IN);
+                run_reduce(x, IN, IN, P, lh, FDEV_REMOTE_Y, FDEV_TAG_STEP);
+            }
+            ftar_drain(c);
+            c->stats.steps++;
         }
-        ftar_drain(c);
-        c->stats.steps++;
+        ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
+        ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
+        ftar_sync_fatal(c);
+        if (x->rank < 2 * x->rem && x->rank % 2 == 0) { /* even: receive the reduced right half (:120) */
+            void *P = ftar_buf(c, c->order[x->rank + 1], WS_IN);
+            run_copy(x, at(x, IN, lh), at(x, P, lh), rh, FDEV_REMOTE_X, FDEV_TAG_STEP);
+            ftar_drain(c);
+        }
+        if (x->vrank != -1)
+            rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+        ftar_sync_fatal(c); /* MPI_Barrier before the tolerant region (:166) */
     }
-    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
-    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
-    ftar_sync_fatal(c);
-    if (x->rank < 2 * x->rem && x->rank % 2 == 0) { /* even: receive the reduced right half (:120) */
-        void *P = ftar_buf(c, c->order[x->rank + 1], WS_IN);
-        run_copy(x, at(x, IN, lh), at(x, P, lh), rh, FDEV_REMOTE_X, FDEV_TAG_STEP);
-        ftar_drain(c);
-    }
-    if (x->vrank != -1)
-        rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
-    ftar_sync_fatal(c); /* MPI_Barrier before the tolerant region (:166) */
 
     /* ---- reduce-scatter (:170-284) ---- */
     int step = 0;
@@ -329,8 +351,8 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             if (x->vrank != -1 && !skip) {
                 const ftar_pull *pl = P.pull[x->rank];
                 void *PIN = ftar_buf(c, pl[0].src, WS_IN);
-                fdev_seg s0 = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, pl[0].off), at(x, IN, pl[0].off),
-                               at(x, PIN, pl[0].off), (size_t)pl[0].n};
+                fdev_seg s0 = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, pl[0].off),
+                               at(x, ftar_local(c, pl[0].x_buf), pl[0].off), at(x, PIN, pl[0].off), (size_t)pl[0].n};
                 fdev_seg s1 = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
                                (size_t)pl[1].n};
                 ftar_run_pulls(c, x->dtype, x->op, &s0, 1, FDEV_TAG_STEP0, 0);
@@ -342,7 +364,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             }
             ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_AFTER);
         } else {
-            ftar_xfer_step(c, &P, x->dtype, x->op, tag, skip, FTAR_PH_LOOP, step, &xs);
+            ftar_xfer_step(c, &P, x->dtype, x->op, tag, skip, FTAR_PH_LOOP, step, NULL, 0, &xs);
         }
         if (step == 0) c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
         ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BARRIER);
@@ -365,7 +387,16 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             skip = ftar_is_dead(c, c->order[rb_real(x, x->vrank ^ mask)]);
             c->stats.steps++;
         }
-        ftar_xfer_step(c, &P, x->dtype, x->op, FDEV_TAG_STEP, skip, FTAR_PH_AG, step, &xs);
+        /* fast_io, last step: this rank's own final half W -> rbuf rides in the same launch */
+        fdev_seg own = {FDEV_COPY, 0, NULL, NULL, NULL, 0};
+        int nown = 0;
+        if (x->fast_io && step == 0) {
+            own.out = at(x, rbuf, x->rindex[0]);
+            own.x = at(x, W, x->rindex[0]);
+            own.n = (size_t)x->rcount[0];
+            nown = 1;
+        }
+        ftar_xfer_step(c, &P, x->dtype, x->op, FDEV_TAG_STEP, skip, FTAR_PH_AG, step, &own, nown, &xs);
         ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BARRIER);
         uint64_t newf = ftar_step_sync(c, 2 * x->steps); /* (:330-335) */
         if (newf) {
@@ -384,6 +415,10 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
     ftar_sync_fatal(c);
+    if (x->fast_io) { /* rbuf is complete; no idle rank reads W, every peer is done with it */
+        ftar_stats_end(c);
+        return FTAR_SUCCESS;
+    }
     if (x->rank < 2 * x->rem && x->rank % 2 != 0) {
         void *P = ftar_buf(c, c->order[x->rank - 1], WS_W); /* odd: result from rank-1 */
         run_copy(x, rbuf, P, (int64_t)count, FDEV_REMOTE_X, FDEV_TAG_STEP);

@@ -244,7 +244,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
         }
         double lb0 = ftar_link_bytes(c);
         ftar_xfer_step(c, &P, x->dtype, x->op, iter == 0 ? FDEV_TAG_STEP0 : FDEV_TAG_STEP, skip, FTAR_PH_LOOP, iter,
-                       &xs);
+                       NULL, 0, &xs);
         if (iter == 0) c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
         if (i >= 0 && !skip) {
             x->cur = out;

@@ -123,17 +123,17 @@ static fdev_seg own_seg(ftar_comm *c, const ftar_pull *pl, int64_t st, int64_t l
     fdev_seg s;
     memset(&s, 0, sizeof(s));
     s.kind = pl->kind;
-    s.out = at(c->ws[pl->dst_buf], st, es);
+    s.out = at(ftar_local(c, pl->dst_buf), st, es);
     s.n = (size_t)len;
     if (pl->kind == FDEV_COPY) {
         s.x = pulled;
         s.remote = FDEV_REMOTE_X;
     } else if (pl->swap) {
         s.x = pulled;
-        s.y = at(c->ws[pl->x_buf], st, es);
+        s.y = at(ftar_local(c, pl->x_buf), st, es);
         s.remote = FDEV_REMOTE_X;
     } else {
-        s.x = at(c->ws[pl->x_buf], st, es);
+        s.x = at(ftar_local(c, pl->x_buf), st, es);
         s.y = pulled;
         s.remote = FDEV_REMOTE_Y;
     }
@@ -195,7 +195,7 @@ void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int n
 }
 
 void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag, int skip, int kphase, int kstep,
-                    ftar_xstate *xs)
+                    const fdev_seg *extra, int nextra, ftar_xstate *xs)
 {
     size_t es = ftar_esize(dtype);
     int me = ftar_my_comm_rank(c);
@@ -203,6 +203,7 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
     xs->skipped = skip;
     fdev_seg segs[FDEV_MAX_SEGS];
     int ns = 0;
+    for (int i = 0; i < nextra; i++) segs[ns++] = extra[i];
     if (!ftar_xfer_would_relay(c, p, es)) { /* direct pull of the whole window */
         if (!skip)
             for (int u = 0; u < p->npull[me]; u++) {

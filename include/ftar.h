@@ -122,8 +122,9 @@ int ftar_set_kills(ftar_comm *comm, const ftar_kill *kills, int nkills);
  */
 
 /* Fault-tolerant Rabenseifner Allreduce (raben/rabenseifner.c:3-395).
- * sbuf is never written (the reference writes through its const sbuf; the build keeps
- * a private device shadow instead).  On recovery the comm is re-targeted in place:
+ * sbuf is never written (the reference writes through its const sbuf; the build stages
+ * what peers read in its own exported buffer); sbuf == rbuf (in place) is allowed.
+ * On recovery the comm is re-targeted in place:
  * ftar_comm_rank/size change exactly as the reference's *comm replacement does. */
 int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count,
                                 ftar_dtype dtype, ftar_op op, ftar_comm *comm);

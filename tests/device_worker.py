@@ -1,0 +1,51 @@
+"""TEST worker: one rank of a device-buffer parity run, launched by ftrun.
+
+Binds the product library through the package (as bench.py does), puts this rank's
+input in a torch tensor on the rank's GPU (optionally at an element offset, optionally
+in place: sbuf == rbuf), calls the device-pointer entry point twice and writes the
+results plus "rc sbuf_untouched" per call for tests/harness.run_torch_worker.
+
+env: FTAR_PROBE_DIR, FTAR_PROBE_ALGO=rd|raben, FTAR_PROBE_INPLACE, FTAR_PROBE_OFFSET
+(set by the harness), FTAR_RANK / FTAR_DEVICE (set by ftrun)
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    d = os.environ["FTAR_PROBE_DIR"]
+    algo = os.environ["FTAR_PROBE_ALGO"]
+    rank = int(os.environ["FTAR_RANK"])
+    inplace = int(os.environ.get("FTAR_PROBE_INPLACE", "0"))
+    off = int(os.environ.get("FTAR_PROBE_OFFSET", "0"))
+    torch.cuda.set_device(int(os.environ.get("FTAR_DEVICE", "0")))
+    spec = importlib.util.spec_from_file_location("ftar_amd", os.path.join(ROOT, "fault-tolerant_amd", "__init__.py"))
+    ftar = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ftar)
+    comm = ftar.Comm.from_env()
+    a = np.fromfile(os.path.join(d, f"in_{rank}.bin"), dtype=np.float32)
+    n = a.size
+    want_in = torch.from_numpy(a)
+    src = torch.zeros(n + off + 16, device="cuda")[off:off + n]
+    for it in range(2):
+        src.copy_(want_in)
+        dst = src if inplace else torch.full((n + off + 16,), float("nan"), device="cuda")[off:off + n]
+        fn = comm.allreduce_rabenseifner if algo == "raben" else comm.recursive_doubling
+        rc = fn(src, dst)
+        torch.cuda.synchronize()
+        untouched = inplace or bool(torch.equal(src.cpu(), want_in))
+        dst.cpu().numpy().tofile(os.path.join(d, f"out_{rank}_{it}.bin"))
+        with open(os.path.join(d, f"status_{rank}_{it}.txt"), "w") as f:
+            f.write(f"{rc} {int(untouched)}\n")
+    comm.finalize()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -116,3 +116,32 @@ def run_driver(which: str, nprocs: int, count: int, backend: str = "hostsim", ki
         if t and t[0] == "Hello":
             hello[int(t[2])] = int(t[-1])
     return cp, hello
+
+
+def run_torch_worker(algo: str, inputs, devmap: str, env_extra: dict | None = None, timeout: int = 300) -> ProbeRun:
+    """Run tests/device_worker.py (torch tensors on the GPU, the device-pointer entry
+    points) as `len(inputs)` ranks under the product's ftrun; two calls per rank."""
+    import sys
+    p = len(inputs)
+    tmp = tempfile.mkdtemp(prefix="ftar_torch_")
+    try:
+        for r, x in enumerate(inputs):
+            np.ascontiguousarray(x, dtype=np.float32).tofile(os.path.join(tmp, f"in_{r}.bin"))
+        env = dict(os.environ, FTAR_PROBE_DIR=tmp, FTAR_PROBE_ALGO=algo)
+        env.pop("FTAR_KILL", None)
+        if env_extra:
+            env.update(env_extra)
+        cmd = [os.path.join(PKG, "bin", "ftrun"), "-np", str(p), "--devmap", devmap, sys.executable, "-u",
+               os.path.join(ROOT, "tests", "device_worker.py")]
+        cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+        outs, stats = {}, {}
+        for r in range(p):
+            for it in range(2):
+                f = os.path.join(tmp, f"out_{r}_{it}.bin")
+                s = os.path.join(tmp, f"status_{r}_{it}.txt")
+                if os.path.exists(f) and os.path.exists(s):
+                    outs.setdefault(r, []).append(np.fromfile(f, dtype=np.float32))
+                    stats.setdefault(r, []).append(tuple(int(v) for v in open(s).read().split()))
+        return ProbeRun(cp.returncode, cp.stdout, cp.stderr, outs, stats)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)

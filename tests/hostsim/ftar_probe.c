@@ -9,7 +9,10 @@
  *
  * env: FTAR_PROBE_DIR, FTAR_PROBE_ALGO=rd|raben, FTAR_PROBE_DTYPE=0..3,
  *      FTAR_PROBE_OP=0..3, FTAR_PROBE_COUNT, FTAR_PROBE_ITERS (default 1),
- *      FTAR_PROBE_DEVICE=1 (device-pointer entry points instead of the host ones)
+ *      FTAR_PROBE_DEVICE=1 (device-pointer entry points on this process's own buffers:
+ *      host-sim build only, where "device" memory is host memory),
+ *      FTAR_PROBE_INPLACE=1 (send buffer = receive buffer),
+ *      FTAR_PROBE_OFFSET=k (buffers start k elements past a 16-byte boundary)
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -28,23 +31,40 @@ int main(void)
     int op = getenv("FTAR_PROBE_OP") ? atoi(getenv("FTAR_PROBE_OP")) : 0;
     size_t count = getenv("FTAR_PROBE_COUNT") ? strtoull(getenv("FTAR_PROBE_COUNT"), NULL, 10) : 0;
     int iters = getenv("FTAR_PROBE_ITERS") ? atoi(getenv("FTAR_PROBE_ITERS")) : 1;
+    int dev = getenv("FTAR_PROBE_DEVICE") ? atoi(getenv("FTAR_PROBE_DEVICE")) : 0;
+    int inplace = getenv("FTAR_PROBE_INPLACE") ? atoi(getenv("FTAR_PROBE_INPLACE")) : 0;
+    size_t off = getenv("FTAR_PROBE_OFFSET") ? strtoull(getenv("FTAR_PROBE_OFFSET"), NULL, 10) : 0;
 
     ftar_comm *comm;
     if (ftar_init(&comm) != FTAR_SUCCESS) return 3;
     int rank;
     ftar_world_rank(comm, &rank);
     size_t bytes = count * esize(dt);
-    void *in = malloc(bytes + 16), *out = malloc(bytes + 16);
+    size_t pad = off * esize(dt);
+    char *in_mem = aligned_alloc(64, (bytes + pad + 64) / 64 * 64), *out_mem = aligned_alloc(64, (bytes + pad + 64) / 64 * 64);
+    void *in = in_mem + pad, *out = out_mem + pad;
     char path[512];
     snprintf(path, sizeof(path), "%s/in_%d.bin", dir, rank);
     FILE *f = fopen(path, "rb");
     if (!f || fread(in, 1, bytes, f) != bytes) return 4;
     fclose(f);
+    void *pristine = malloc(bytes ? bytes : 1);
+    memcpy(pristine, in, bytes);
     for (int it = 0; it < iters; it++) {
         memset(out, 0xEE, bytes);
-        int rc = !strcmp(algo, "rd") ? ftar_recursive_doubling_host(in, out, count, (ftar_dtype)dt, (ftar_op)op, comm)
-                                     : ftar_allreduce_rabenseifner_host(in, out, count, (ftar_dtype)dt,
-                                                                        (ftar_op)op, comm);
+        const void *src = in;
+        if (inplace) {
+            memcpy(out, in, bytes);
+            src = out;
+        }
+        int rd = !strcmp(algo, "rd"), rc;
+        if (dev)
+            rc = rd ? ftar_recursive_doubling(src, out, count, (ftar_dtype)dt, (ftar_op)op, comm)
+                    : ftar_allreduce_rabenseifner(src, out, count, (ftar_dtype)dt, (ftar_op)op, comm);
+        else
+            rc = rd ? ftar_recursive_doubling_host(src, out, count, (ftar_dtype)dt, (ftar_op)op, comm)
+                    : ftar_allreduce_rabenseifner_host(src, out, count, (ftar_dtype)dt, (ftar_op)op, comm);
+        if (!inplace && memcmp(in, pristine, bytes) != 0) rc = 99; /* the send buffer was written */
         int crank = -1, csize = -1;
         ftar_comm_rank(comm, &crank);
         ftar_comm_size(comm, &csize);
@@ -61,5 +81,8 @@ int main(void)
         fclose(f);
     }
     ftar_finalize(comm);
+    free(pristine);
+    free(in_mem);
+    free(out_mem);
     return 0;
 }

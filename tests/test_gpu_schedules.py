@@ -171,3 +171,22 @@ def test_raben_redundancy_always(oracle, p, kill):
     """The reference's step-0 full exchange kept at power-of-two p (FTAR_REDUNDANCY=1)."""
     _check(oracle.rabenseifner, "raben", oracle.random_inputs(p, 100003, seed=p + 70),
            [kill] if kill else [], env={"FTAR_REDUNDANCY": "1"})
+
+
+@pytest.mark.parametrize("algo,p,mode", [("raben", 4, "plain"), ("raben", 4, "inplace"), ("raben", 2, "offset1"),
+                                         ("raben", 8, "inplace_offset3"), ("raben", 3, "inplace"),
+                                         ("rd", 4, "inplace"), ("rd", 4, "offset1")])
+def test_torch_device_buffers(oracle, algo, p, mode):
+    """The device-pointer entry points on torch tensors (bench.py's path), bound through
+    the Python package: in place, at element offsets, two calls; sbuf untouched."""
+    env = {"plain": {}, "inplace": {"FTAR_PROBE_INPLACE": "1"}, "offset1": {"FTAR_PROBE_OFFSET": "1"},
+           "inplace_offset3": {"FTAR_PROBE_INPLACE": "1", "FTAR_PROBE_OFFSET": "3"}}[mode]
+    ins = oracle.random_inputs(p, 65536 + 17, seed=p + 90)
+    o = (oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling)(ins)
+    r = H.run_torch_worker(algo, ins, devmap=ALL_ON_GPU0, env_extra=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for w in range(p):
+        assert len(r.outputs.get(w, [])) == 2, r.stderr[-2000:]
+        for it in range(2):
+            assert r.status[w][it] == (0, 1), (w, it, r.status[w][it])
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)

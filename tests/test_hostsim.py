@@ -273,3 +273,29 @@ def test_campaign_sizes(hostsim, oracle, algo, p):
     for _ in range(3):
         k = (rng.randrange(p), rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(steps), 2)
         _cmp(fn, algo, ins, [k])
+
+
+DEVICE_MODES = {"plain": {}, "inplace": {"FTAR_PROBE_INPLACE": "1"}, "offset1": {"FTAR_PROBE_OFFSET": "1"},
+                "inplace_offset3": {"FTAR_PROBE_INPLACE": "1", "FTAR_PROBE_OFFSET": "3"}}
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [1, 2, 4, 5, 8])
+@pytest.mark.parametrize("mode", sorted(DEVICE_MODES))
+@pytest.mark.parametrize("relay", [False, True])
+def test_device_entry_points(hostsim, oracle, algo, p, mode, relay):
+    """The device-pointer entry points (what bench.py and torch callers use) on the
+    caller's own buffers: in place (sbuf == rbuf), buffers not co-aligned with the
+    workspace, two calls per job; sbuf is never written (the probe checks it).  At
+    power-of-two p Raben reads sbuf and writes rbuf in place (fast_io)."""
+    env = dict(DEVICE_MODES[mode], FTAR_PROBE_DEVICE="1")
+    if relay:
+        env["FTAR_RELAY_MIN"] = "0"
+    ins = oracle.random_inputs(p, 1031, seed=p + 80)
+    o = _fn(oracle, algo)(ins)
+    r = H.run_probe(algo, ins, iters=2, backend="hostsim", env_extra=env)
+    assert r.returncode == 0, r.stderr[-1000:]
+    for w in range(p):
+        for it in range(2):
+            assert r.status[w][it][0] == 0, (w, it, r.status[w][it])
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
