@@ -37,6 +37,7 @@ typedef struct {
     const void *x;
     const void *y;
     size_t n;         /* elements */
+    void *out2;       /* optional second destination receiving the same values (local) */
 } fdev_seg;
 
 #define FDEV_MAX_SEGS 16 /* a relayed exchange step: 2 own pulls + 2 x 6 relay duties */

@@ -218,12 +218,13 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
         in[i].x = segs[i].x;
         in[i].y = segs[i].y;
         in[i].n = segs[i].n;
+        in[i].out2 = segs[i].out2;
         double b = (double)segs[i].n * (double)es;
         int nread = segs[i].kind == FDEV_COPY ? 1 : 2;
         int nremote = ((segs[i].remote & FDEV_REMOTE_X) ? 1 : 0) +
                       ((segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) ? 1 : 0);
         d->ctr.link_bytes += b * nremote;
-        d->ctr.hbm_bytes += b * (1 + nread - nremote);
+        d->ctr.hbm_bytes += b * (1 + nread - nremote + (segs[i].out2 ? 1 : 0));
     }
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
@@ -416,7 +417,7 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
         return 0;
     }
     // MPI_Reduce_local(in, inout): inout = inout <op> in  -> x = inout, y = in
-    ftar::SegIn seg{ftar::kReduce, inout, inout, in, n};
+    ftar::SegIn seg{ftar::kReduce, inout, inout, in, n, nullptr};
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(&seg, 1, es, cached_blocks, &L);
     if (grid == 0) return 0;

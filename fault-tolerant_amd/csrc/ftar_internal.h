@@ -116,6 +116,7 @@ typedef struct {
     int src, src_buf;
     int dst_buf, x_buf;
     int64_t off, n;
+    int to_uout; /* also store the result in the caller's output buffer (same offset) */
 } ftar_pull;
 
 #define FTAR_MAX_PULLS 2

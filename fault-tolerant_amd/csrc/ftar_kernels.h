@@ -17,6 +17,7 @@ constexpr int kMaxIleave = 16; // vector pieces that can share the interleaved p
 
 struct KSeg {
     void *out;
+    void *out2;          // optional second destination (same values), nullptr = none
     const void *x;
     const void *y;
     size_t n;
@@ -75,6 +76,7 @@ struct SegIn {
     const void *x;
     const void *y;
     size_t n;
+    void *out2;
 };
 
 unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_blocks, KSegList *L);

@@ -91,6 +91,7 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk)
     const uint4 *__restrict__ X = (const uint4 *)S.x;
     const uint4 *__restrict__ Y = (const uint4 *)S.y;
     uint4 *__restrict__ O = (uint4 *)S.out;
+    uint4 *__restrict__ O2 = (uint4 *)S.out2; // wave-uniform: both stores or one
     const size_t nv = S.n / E;
     for (size_t base = b * kTile; base < nv; base += nblk * kTile) {
         const size_t i = base + threadIdx.x;
@@ -98,18 +99,24 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk)
             uint4 a[kUnroll], c[kUnroll];
 #pragma unroll
             for (int u = 0; u < kUnroll; u++) a[u] = ldnt(X + i + u * kBlock);
-            if (S.kind == kCopy) {
-#pragma unroll
-                for (int u = 0; u < kUnroll; u++) O[i + u * kBlock] = a[u];
-            } else {
+            if (S.kind != kCopy) {
 #pragma unroll
                 for (int u = 0; u < kUnroll; u++) c[u] = ldnt(Y + i + u * kBlock);
 #pragma unroll
-                for (int u = 0; u < kUnroll; u++) O[i + u * kBlock] = apply16<T, OP>(a[u], c[u]);
+                for (int u = 0; u < kUnroll; u++) a[u] = apply16<T, OP>(a[u], c[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; u++) O[i + u * kBlock] = a[u];
+            if (O2) {
+#pragma unroll
+                for (int u = 0; u < kUnroll; u++) O2[i + u * kBlock] = a[u];
             }
         } else {
-            for (size_t j = i; j < nv; j += kBlock)
-                O[j] = (S.kind == kCopy) ? ldnt(X + j) : apply16<T, OP>(ldnt(X + j), ldnt(Y + j));
+            for (size_t j = i; j < nv; j += kBlock) {
+                const uint4 v = (S.kind == kCopy) ? ldnt(X + j) : apply16<T, OP>(ldnt(X + j), ldnt(Y + j));
+                O[j] = v;
+                if (O2) O2[j] = v;
+            }
         }
     }
 }
@@ -120,9 +127,13 @@ __device__ __forceinline__ void scalar_body(const KSeg &S, size_t b, size_t nblk
     const T *X = (const T *)S.x;
     const T *Y = (const T *)S.y;
     T *O = (T *)S.out;
+    T *O2 = (T *)S.out2;
     const size_t stride = nblk * kBlock;
-    for (size_t i = b * kBlock + threadIdx.x; i < S.n; i += stride)
-        O[i] = (S.kind == kCopy) ? X[i] : apply<T, OP>(X[i], Y[i]);
+    for (size_t i = b * kBlock + threadIdx.x; i < S.n; i += stride) {
+        const T v = (S.kind == kCopy) ? X[i] : apply<T, OP>(X[i], Y[i]);
+        O[i] = v;
+        if (O2) O2[i] = v;
+    }
 }
 
 template <typename T, int OP>
@@ -237,8 +248,9 @@ unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_bloc
         const SegIn &g = in[s];
         if (g.n == 0) continue;
         uintptr_t ao = (uintptr_t)g.out, ax = (uintptr_t)g.x, ay = (uintptr_t)(g.kind == kCopy ? g.x : g.y);
-        bool co = ((ao & 15) == (ax & 15)) && ((ao & 15) == (ay & 15)) && (16 % esize == 0) &&
-                  ((ao & 15) % esize == 0);
+        uintptr_t ao2 = g.out2 ? (uintptr_t)g.out2 : ao;
+        bool co = ((ao & 15) == (ax & 15)) && ((ao & 15) == (ay & 15)) && ((ao & 15) == (ao2 & 15)) &&
+                  (16 % esize == 0) && ((ao & 15) % esize == 0);
         size_t head = 0, body = 0;
         if (co) {
             size_t mis = ao & 15;
@@ -253,6 +265,7 @@ unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_bloc
             if (n == 0) return;
             KSeg k;
             k.out = (char *)g.out + off * esize;
+            k.out2 = g.out2 ? (void *)((char *)g.out2 + off * esize) : nullptr;
             k.x = (const char *)g.x + off * esize;
             k.y = g.kind == kCopy ? k.x : (const void *)((const char *)g.y + off * esize);
             k.n = n;

@@ -41,6 +41,7 @@ typedef struct {
     int keep_recov; /* step 0 also pulls the partner's other half into T (recovery data) */
     int bg_pending; /* step-0 redundancy copy still running on the background stream */
     int fast_io;    /* power of two, no recovery data: sbuf/rbuf used in place (see below) */
+    int out_done;   /* the last allgather step already stored this rank's result in rbuf */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
 } rb_ctx;
 
@@ -103,16 +104,17 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
         int src = c->order[rb_real(x, v ^ mask)];
         ftar_pull *pl = P->pull[cr];
         memset(pl, 0, sizeof(ftar_pull) * FTAR_MAX_PULLS);
-        if (ag) { /* fast_io: the last allgather step lands in rbuf */
-            int dst = (x->fast_io && step == 0) ? WS_UOUT : WS_W;
-            pl[0] = (ftar_pull){FDEV_COPY, 0, src, WS_W, dst, WS_W, si[step], sc[step]};
+        if (ag) { /* the last allgather step lands in rbuf: only there (fast_io) or also in W */
+            int last = step == 0;
+            pl[0] = (ftar_pull){FDEV_COPY, 0, src, WS_W, (x->fast_io && last) ? WS_UOUT : WS_W, WS_W, si[step],
+                                sc[step], !x->fast_io && last};
             P->npull[cr] = 1;
         } else if (step == 0) { /* fast_io: the local operand is sbuf itself */
-            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, x->fast_io ? WS_UIN : WS_IN, ri[0], rc[0]};
-            pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0]};
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, x->fast_io ? WS_UIN : WS_IN, ri[0], rc[0], 0};
+            pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0], 0};
             P->npull[cr] = x->keep_recov ? 2 : 1;
         } else {
-            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_W, WS_W, WS_W, ri[step], rc[step]};
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_W, WS_W, WS_W, ri[step], rc[step], 0};
             P->npull[cr] = 1;
         }
     }
@@ -120,13 +122,13 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
 
 static void run_reduce(rb_ctx *x, void *out, const void *xin, const void *yin, int64_t n, int remote, int tag)
 {
-    fdev_seg s = {FDEV_REDUCE, remote, out, xin, yin, (size_t)n};
+    fdev_seg s = {FDEV_REDUCE, remote, out, xin, yin, (size_t)n, NULL};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
 static void run_copy(rb_ctx *x, void *out, const void *src, int64_t n, int remote, int tag)
 {
-    fdev_seg s = {FDEV_COPY, remote, out, src, NULL, (size_t)n};
+    fdev_seg s = {FDEV_COPY, remote, out, src, NULL, (size_t)n, NULL};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
@@ -352,9 +354,10 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                 const ftar_pull *pl = P.pull[x->rank];
                 void *PIN = ftar_buf(c, pl[0].src, WS_IN);
                 fdev_seg s0 = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, pl[0].off),
-                               at(x, ftar_local(c, pl[0].x_buf), pl[0].off), at(x, PIN, pl[0].off), (size_t)pl[0].n};
+                               at(x, ftar_local(c, pl[0].x_buf), pl[0].off), at(x, PIN, pl[0].off), (size_t)pl[0].n,
+                               NULL};
                 fdev_seg s1 = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
-                               (size_t)pl[1].n};
+                               (size_t)pl[1].n, NULL};
                 ftar_run_pulls(c, x->dtype, x->op, &s0, 1, FDEV_TAG_STEP0, 0);
                 if (x->keep_recov) {
                     ftar_run_pulls(c, x->dtype, x->op, &s1, 1, FDEV_TAG_BG, 1);
@@ -387,10 +390,10 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             skip = ftar_is_dead(c, c->order[rb_real(x, x->vrank ^ mask)]);
             c->stats.steps++;
         }
-        /* fast_io, last step: this rank's own final half W -> rbuf rides in the same launch */
-        fdev_seg own = {FDEV_COPY, 0, NULL, NULL, NULL, 0};
+        /* last step: this rank's own final half W -> rbuf rides in the same launch */
+        fdev_seg own = {FDEV_COPY, 0, NULL, NULL, NULL, 0, NULL};
         int nown = 0;
-        if (x->fast_io && step == 0) {
+        if (step == 0 && x->vrank != -1) {
             own.out = at(x, rbuf, x->rindex[0]);
             own.x = at(x, W, x->rindex[0]);
             own.n = (size_t)x->rcount[0];
@@ -399,6 +402,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         ftar_xfer_step(c, &P, x->dtype, x->op, FDEV_TAG_STEP, skip, FTAR_PH_AG, step, &own, nown, &xs);
         ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BARRIER);
         uint64_t newf = ftar_step_sync(c, 2 * x->steps); /* (:330-335) */
+        x->out_done = nown && !skip && !newf; /* a recovery here re-homes windows: copy W at the end */
         if (newf) {
             ftar_xfer_repair(c, &P, x->dtype, x->op, &xs, newf);
             rb_handler_ag(x, newf, step);
@@ -423,7 +427,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         void *P = ftar_buf(c, c->order[x->rank - 1], WS_W); /* odd: result from rank-1 */
         run_copy(x, rbuf, P, (int64_t)count, FDEV_REMOTE_X, FDEV_TAG_STEP);
         c->stats.steps++;
-    } else { /* with one rank there is no exchange and rbuf = sbuf (:35-42) */
+    } else if (!x->out_done) { /* with one rank there is no exchange and rbuf = sbuf (:35-42) */
         run_copy(x, rbuf, x->steps == 0 ? IN : W, (int64_t)count, 0, FDEV_TAG_LOCAL);
     }
     ftar_drain(c);

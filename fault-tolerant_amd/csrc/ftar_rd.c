@@ -56,7 +56,7 @@ static int peer_cur(rd_ctx *x, int w) { return (int)ftar_peer_pub(x->c, w); }
 
 static void run1(rd_ctx *x, int kind, void *out, const void *a, const void *b, int remote, int tag)
 {
-    fdev_seg s = {kind, remote, out, a, b, x->count};
+    fdev_seg s = {kind, remote, out, a, b, x->count, NULL};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
@@ -176,6 +176,8 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     if (x->es == 0 || op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
     if (count && (!src || !dst)) return FTAR_ERR_ARG;
     if (count == 0) return FTAR_SUCCESS;
+    c->uin = src;
+    c->uout = dst;
     ftar_stats_begin(c);
     int me = c->wrank;
 
@@ -214,7 +216,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     if (newf & involved) ftar_abort(c, FTAR_ERR_PROC_FAILED);
 
     /* recursive doubling body (:21-71) */
-    int iter = 0;
+    int iter = 0, dst_done = 0;
     for (int distance = 1; distance < x->nactive; distance *= 2, iter++) {
         int last = (distance * 2 >= x->nactive);
         int i = index_of(x->active, x->nactive, me);
@@ -229,10 +231,11 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
             int cr = ftar_comm_rank_of(c, x->active[a]);
             int pw = x->active[a ^ distance];
             ftar_pull *pl = &P.pull[cr][0];
-            *pl = (ftar_pull){FDEV_REDUCE, last, pw, peer_cur(x, pw), 0, 0, 0, (int64_t)count};
+            *pl = (ftar_pull){FDEV_REDUCE, last, pw, peer_cur(x, pw), 0, 0, 0, (int64_t)count, 0};
             if (a == i) {
                 pl->dst_buf = out;
                 pl->x_buf = x->cur;
+                pl->to_uout = last; /* the result also lands in dst (no final copy) */
             }
             P.npull[cr] = 1;
         }
@@ -252,6 +255,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
         }
         ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BARRIER);
         newf = ftar_step_sync(c, ftar_hibit(x->nactive, 31) > 0 ? ftar_hibit(x->nactive, 31) : 1); /* (:51-53) */
+        dst_done = last && i >= 0 && !skip && !newf; /* a recovery may move on: copy at the end */
         if (newf) {
             ftar_xfer_repair(c, &P, x->dtype, x->op, &xs, newf);
             int dd = rd_handler(x, newf, distance * 2);
@@ -270,7 +274,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
         int from = x->active[ii];
         run1(x, FDEV_COPY, dst, ftar_buf(c, from, peer_cur(x, from)), NULL, FDEV_REMOTE_X, FDEV_TAG_STEP);
         c->stats.steps++;
-    } else {
+    } else if (!dst_done) {
         run1(x, FDEV_COPY, dst, c->ws[x->cur], NULL, 0, FDEV_TAG_LOCAL);
     }
     ftar_drain(c);

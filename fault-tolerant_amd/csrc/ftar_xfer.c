@@ -124,6 +124,7 @@ static fdev_seg own_seg(ftar_comm *c, const ftar_pull *pl, int64_t st, int64_t l
     memset(&s, 0, sizeof(s));
     s.kind = pl->kind;
     s.out = at(ftar_local(c, pl->dst_buf), st, es);
+    if (pl->to_uout) s.out2 = at(c->uout, st, es);
     s.n = (size_t)len;
     if (pl->kind == FDEV_COPY) {
         s.x = pulled;
@@ -170,6 +171,8 @@ void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int n
             local[nl++] = t;
         } else if (t.kind == FDEV_COPY) {
             rc = fdev_copy(c->dev, bg, t.out, t.x, t.n * es, 1, tag);
+            if (t.out2) /* the second destination from the landed copy (same stream) */
+                local[nl++] = (fdev_seg){FDEV_COPY, 0, t.out2, t.out, NULL, t.n, NULL};
         } else {
             void *stage = staging_of(c, t.out);
             if (!stage) {

@@ -160,14 +160,15 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
         const fdev_seg *s = &segs[k];
         if (s->kind == FDEV_COPY) {
             memmove(s->out, s->x, s->n * esz(dtype));
-            continue;
+        } else {
+            switch (dtype) {
+            case 0: LOOP(int32_t, uint32_t); break;
+            case 1: LOOP(float, float); break;
+            case 2: LOOP(int64_t, uint64_t); break;
+            default: LOOP(double, double); break;
+            }
         }
-        switch (dtype) {
-        case 0: LOOP(int32_t, uint32_t); break;
-        case 1: LOOP(float, float); break;
-        case 2: LOOP(int64_t, uint64_t); break;
-        default: LOOP(double, double); break;
-        }
+        if (s->out2) memmove(s->out2, s->out, s->n * esz(dtype));
     }
     d->ctr.launches[tag]++;
     return 0;
@@ -214,7 +215,7 @@ int fdev_set_reduce_variant(int v) { return 0; }
 
 int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream)
 {
-    fdev_seg s = {FDEV_REDUCE, 0, inout, inout, in, n};
+    fdev_seg s = {FDEV_REDUCE, 0, inout, inout, in, n, NULL};
     ftar_dev d;
     memset(&d, 0, sizeof(d));
     return fdev_run(&d, dtype, op, &s, 1, 0);

@@ -52,6 +52,7 @@ int main(int argc, char **argv)
             in[i].x = (const void *)(base + ((uintptr_t)1 << 36) + mis_x);
             in[i].y = (const void *)(base + ((uintptr_t)2 << 36) + mis_o);
             in[i].n = n;
+            in[i].out2 = (rnd() % 4 == 0) ? (void *)(base + ((uintptr_t)3 << 36) + mis_o) : nullptr;
         }
         unsigned max_blocks = (rnd() % 5 == 0) ? 64 + (unsigned)(rnd() % 2048) : 262144;
         KSegList L;
