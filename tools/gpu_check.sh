@@ -48,6 +48,19 @@ if [[ $STEPS == *rehearse* ]]; then
     rc=$?; cat "$OUT/rehearse_$n.json"; tail -3 "$OUT/rehearse_$n.err"; stop_on_fault $rc rehearse_$n
   done
 fi
+if [[ $STEPS == *sweep* ]]; then
+  # per-call time over message sizes, 2 / 4 / 8 ranks sharing GPU 0
+  for n in ${SWEEP_RANKS:-2 4 8}; do
+    timeout -k 10 300 fault-tolerant_amd/bin/ftrun -np $n --devmap 0,0,0,0,0,0,0,0 python -u tools/size_sweep.py \
+        "$OUT/sweep_$n.json" > "$OUT/sweep_$n.log" 2>&1
+    rc=$?; tail -2 "$OUT/sweep_$n.log"; stop_on_fault $rc sweep_$n
+  done
+fi
+if [[ $STEPS == *syncprobe* ]]; then
+  # device round trip of one step: kernel + marker event + host spin (tools/sync_probe.hip)
+  timeout -k 10 120 tools/_build/sync_probe > "$OUT/sync_probe.json" 2>&1
+  rc=$?; cat "$OUT/sync_probe.json"; stop_on_fault $rc syncprobe
+fi
 if [[ $STEPS == *cpubase* ]]; then
   # CPU baseline of the schedules on this box's host cores (no GPU involved)
   timeout -k 10 900 python tools/cpu_schedule_bench.py --out "$OUT/cpu_schedule_bench.json" > "$OUT/cpubase.log" 2>&1
