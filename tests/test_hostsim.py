@@ -189,7 +189,7 @@ def test_relay_nofault_parity(hostsim, oracle, algo, p):
         assert min(relayed) > 0, relayed
 
 
-@pytest.mark.parametrize("algo,p", [("raben", 5), ("raben", 9), ("rd", 4), ("rd", 8), ("rd", 6)])
+@pytest.mark.parametrize("algo,p", [("raben", 5), ("raben", 8), ("raben", 9), ("rd", 4), ("rd", 8), ("rd", 6)])
 def test_relay_single_kill_sweep(hostsim, oracle, algo, p):
     """Relays that die before or after forwarding, partners that die mid-step: same
     outcomes and bits as the oracle (lost stripes are re-pulled before the handler)."""
@@ -229,7 +229,7 @@ def test_copy_engine_nofault_parity(hostsim, oracle, algo, p):
     _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 4099, seed=p + 7), env=CE)
 
 
-@pytest.mark.parametrize("algo,p", [("raben", 9), ("rd", 8), ("rd", 6)])
+@pytest.mark.parametrize("algo,p", [("raben", 8), ("raben", 9), ("rd", 8), ("rd", 6)])
 def test_copy_engine_single_kill_sweep(hostsim, oracle, algo, p):
     ins = oracle.random_inputs(p, 1031, seed=p + 3)
     fn = _fn(oracle, algo)
