@@ -17,6 +17,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HOSTSIM = os.path.join(ROOT, "tests", "hostsim", "_build")
+# the same host-sim build with AddressSanitizer + UndefinedBehaviorSanitizer (test_sanitizers.py)
+HOSTSIM_ASAN = os.path.join(ROOT, "tests", "hostsim", "_build_asan")
 PKG = os.path.join(ROOT, "fault-tolerant_amd")
 
 
@@ -48,9 +50,10 @@ def run_probe(algo: str, inputs, kills=(), op: int = 0, iters: int = 1, backend:
     try:
         for r, x in enumerate(inputs):
             np.ascontiguousarray(x).tofile(os.path.join(tmp, f"in_{r}.bin"))
-        if backend == "hostsim":
-            ftrun = os.path.join(HOSTSIM, "bin", "ftrun")
-            probe = os.path.join(HOSTSIM, "bin", "ftar_probe")
+        if backend in ("hostsim", "hostsim_asan"):
+            hs = HOSTSIM if backend == "hostsim" else HOSTSIM_ASAN
+            ftrun = os.path.join(hs, "bin", "ftrun")
+            probe = os.path.join(hs, "bin", "ftar_probe")
         else:
             ftrun = os.path.join(PKG, "bin", "ftrun")
             probe = os.path.join(HOSTSIM, "gpu", "ftar_probe")
