@@ -218,22 +218,35 @@ def multi(args):
         finally:
             args.steps, args.warmup = saved
 
-    # Transport selection before the timed run: the relay transport's gain depends on
-    # how the node's xGMI links behave under concurrent peer reads, so a short
-    # comparison (max over ranks, identical on every rank) picks relay or direct.
+    # Transport selection before the timed run: how the node's xGMI links behave under
+    # concurrent peer reads decides between the one-hop mesh (power-of-two p without a
+    # spare), the 2-hop relay and plain pairwise pulls, so a short comparison (max over
+    # ranks, identical on every rank) picks one.  All three give the same bits.
     selection = None
-    if world >= 3 and not args.no_variants and comm.get_option(ftar.OPT_RELAY):
-        t_relay = quick(raben)
-        comm.set_option(ftar.OPT_RELAY, 0)
-        t_direct = quick(raben)
-        chosen = "relay2hop" if t_relay <= t_direct else "direct"
-        comm.set_option(ftar.OPT_RELAY, 1 if chosen == "relay2hop" else 0)
-        selection = {"relay2hop_ms": round(t_relay * 1e3, 4), "direct_ms": round(t_direct * 1e3, 4),
-                     "chosen": chosen}
+    pow2 = world & (world - 1) == 0
+    if world >= 2 and not args.no_variants:
+        cands = {}
+        if pow2 and comm.get_option(ftar.OPT_MESH):
+            cands["mesh"] = (1, 1)
+        if world >= 3 and comm.get_option(ftar.OPT_RELAY):
+            cands["relay2hop"] = (0, 1)
+        cands["direct"] = (0, 0)
+        if len(cands) > 1:
+            times = {}
+            for name, (m, r) in cands.items():
+                comm.set_option(ftar.OPT_MESH, m)
+                comm.set_option(ftar.OPT_RELAY, r)
+                times[name] = quick(raben)
+            chosen = min(times, key=times.get)
+            comm.set_option(ftar.OPT_MESH, cands[chosen][0])
+            comm.set_option(ftar.OPT_RELAY, cands[chosen][1])
+            selection = {f"{k}_ms": round(t * 1e3, 4) for k, t in times.items()}
+            selection["chosen"] = chosen
 
     t_rb, k_rb = timed(raben)
     step0_bytes = timed.link_bytes
     relayed = comm.last_stats().relayed_steps > 0
+    meshed = comm.last_stats().mesh_steps > 0
     # correctness spot check against torch.distributed's all_reduce on the same inputs
     # (fp32, different reduction order: |err| <= log2(p) * 2^-24 * sum|x_i|)
     ref = x.clone() if args.dist_backend == "nccl" else x.cpu()
@@ -255,20 +268,22 @@ def multi(args):
     # without the background-stream redundancy copy -- the reference's transport shape
     transports = {}
     if not args.no_variants:
-        opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY)
+        opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY, ftar.OPT_MESH)
         defaults = {o: comm.get_option(o) for o in opts}
-        # direct: one pull kernel per step; direct_serial: plus the step-0 copy inline;
-        # copy_engine: hipMemcpyAsync of the partner's window + a local reduce kernel;
-        # reference_shape: pairwise, inline, with the step-0 full exchange even where no
-        # handler can use it (the reference's data movement); relay_full_exchange: the
-        # default transport with that full exchange
-        variants = (("direct", (0, 1, 0, 0)), ("direct_serial", (0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0)),
-                    ("reference_shape", (0, 0, 0, 1)), ("relay_full_exchange", (1, 1, 0, 1)))
+        # mesh: one-hop reduce-scatter + allgather (power-of-two p, no spare); relay2hop:
+        # the step-by-step schedule striped over 2-hop paths; direct: one pull kernel per
+        # step; direct_serial: plus the step-0 copy inline; copy_engine: hipMemcpyAsync of
+        # the partner's window + a local reduce kernel; reference_shape: pairwise, inline,
+        # with the step-0 full exchange even where no handler can use it (the reference's
+        # data movement); relay_full_exchange: the relay with that full exchange
+        variants = (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
+                    ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
+                    ("reference_shape", (0, 0, 0, 1, 0)), ("relay_full_exchange", (1, 1, 0, 1, 0)))
         for name, vals in variants:
             for o, v in zip(opts, vals):
                 comm.set_option(o, v)
             tv, _ = timed(raben)
-            tv_rd, _ = timed(rd) if name in ("direct", "copy_engine") else (None, None)
+            tv_rd, _ = timed(rd) if name in ("relay2hop", "direct", "copy_engine") else (None, None)
             transports[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2)}
             if tv_rd:
                 transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
@@ -306,14 +321,17 @@ def multi(args):
     classic = 2 * (1 - 2.0 ** -L) * S
     keep = world != r or comm.get_option(ftar.OPT_REDUNDANCY) != 0
     sched_bytes = ft_bytes if keep else classic
-    if relayed:
+    if meshed:
+        # one hop over p - 1 links: S/p per link for each of reduce-scatter and allgather
+        t_roof = 2.0 * S / world / (XGMI_LINK_GBS * 1e9)
+    elif relayed:
         t_roof = 2.0 / r * sched_bytes / (XGMI_LINK_GBS * 1e9)
     elif comm.get_option(ftar.OPT_OVERLAP) != 0:
         t_roof = classic / (XGMI_LINK_GBS * 1e9)
     else:
         t_roof = sched_bytes / (XGMI_LINK_GBS * 1e9)
     t_survey = ft_bytes / (XGMI_LINK_GBS * 1e9)  # the FT schedule on one link per step
-    links = (r - 1) if relayed else 1
+    links = (world - 1) if meshed else (r - 1) if relayed else 1
     peak = links * XGMI_LINK_GBS
     achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernels' pulled bytes
     if rank == 0:
@@ -326,7 +344,7 @@ def multi(args):
                                    "rank, one rank per MI355X, pull exchanges over xGMI",
                        "count": args.count, "parallelism": f"{world} ranks"},
             "algbw_GBps": round(S / t_rb / 1e9, 2),
-            "transport": "relay2hop" if relayed else "direct",
+            "transport": "mesh" if meshed else "relay2hop" if relayed else "direct",
             "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "link_GBps": XGMI_LINK_GBS,
                                        "links_per_step": links, "t_roof_ms": round(t_roof * 1e3, 3),
                                        "frac": round(t_roof / t_rb, 4),
@@ -335,7 +353,8 @@ def multi(args):
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
                          "peak": peak, "unit": "GB/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
-                         "kernel": ("Raben RS step 0, both relay phases (stripes pulled over r-1 links)" if relayed
+                         "kernel": ("Raben mesh reduce-scatter: tree_kernel over p-1 one-hop pulls" if meshed
+                                    else "Raben RS step 0, both relay phases (stripes pulled over r-1 links)" if relayed
                                     else "Raben RS step 0 reduce half (pull partner's half, reduce into W)"),
                          "algorithmic_bytes_per_launch": step0_bytes, "kernel_ms": round(k_rb, 4)},
             "e2e_host_buffers": {"ms_per_step": round(t_e2e * 1e3, 3), "algbw_GBps": round(S / t_e2e / 1e9, 2)},

@@ -24,7 +24,7 @@ INT32, FLOAT32, INT64, FLOAT64 = 0, 1, 2, 3
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
 PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
 PT_BEFORE, PT_AFTER, PT_BARRIER = 0, 1, 2
-OPT_OVERLAP, OPT_RELAY, OPT_RELAY_MIN, OPT_LOOP_SECONDS, OPT_COPY_ENGINE, OPT_REDUNDANCY = 0, 1, 2, 3, 4, 5
+OPT_OVERLAP, OPT_RELAY, OPT_RELAY_MIN, OPT_LOOP_SECONDS, OPT_COPY_ENGINE, OPT_REDUNDANCY, OPT_MESH = 0, 1, 2, 3, 4, 5, 6
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
 
 
@@ -38,7 +38,8 @@ class Stats(ctypes.Structure):
                 ("step0_kernel_ms", ctypes.c_double), ("link_bytes", ctypes.c_double),
                 ("hbm_bytes", ctypes.c_double), ("kernels", ctypes.c_int), ("step0_link_bytes", ctypes.c_double),
                 ("bg_kernel_ms", ctypes.c_double), ("sync_wait_s", ctypes.c_double),
-                ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int), ("relayed_steps", ctypes.c_int)]
+                ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int), ("relayed_steps", ctypes.c_int),
+                ("mesh_steps", ctypes.c_int)]
 
 
 class Kill(ctypes.Structure):

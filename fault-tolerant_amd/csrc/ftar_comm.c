@@ -128,6 +128,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->relay = getenv("FTAR_RELAY") ? atoi(getenv("FTAR_RELAY")) : 1;
     c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 0;
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
+    c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
     c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)4 << 20);
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
@@ -268,6 +269,7 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_LOOP_SECONDS: c->loop_seconds = v; break;
     case FTAR_OPT_COPY_ENGINE: c->copy_engine = v != 0; break;
     case FTAR_OPT_REDUNDANCY: c->redundancy = v != 0; break;
+    case FTAR_OPT_MESH: c->mesh = v != 0; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;
@@ -283,6 +285,7 @@ int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
     case FTAR_OPT_LOOP_SECONDS: *v = c->loop_seconds; break;
     case FTAR_OPT_COPY_ENGINE: *v = c->copy_engine; break;
     case FTAR_OPT_REDUNDANCY: *v = c->redundancy; break;
+    case FTAR_OPT_MESH: *v = c->mesh; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;

@@ -71,6 +71,12 @@ int fdev_unimport(ftar_dev *d, void *ptr);
 
 /* Enqueue one segment kernel on the rank's stream. */
 int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+/* Tree reduce of nsrc (2, 4, 8 or 16) sources into out on the rank's stream:
+ * out[i] = ((src0 op src1) op (src2 op src3)) op ...; bit j of remote_mask marks src[j]
+ * as a peer mapping (byte accounting). */
+#define FDEV_MAX_TREE 16
+int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
+              size_t n, int tag);
 /* Enqueue on the rank's background stream, ordered after everything queued so far on
  * the main stream (it then overlaps later main-stream work). */
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);

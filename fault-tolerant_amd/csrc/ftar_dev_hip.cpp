@@ -244,6 +244,48 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
     return 0;
 }
 
+int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
+              size_t n, int tag)
+{
+    size_t es = esize_of(dtype);
+    if (es == 0 || op < 0 || op > 3 || tag < 0 || tag >= FDEV_NTAGS ||
+        !(nsrc == 2 || nsrc == 4 || nsrc == 8 || nsrc == 16)) {
+        snprintf(g_err, sizeof(g_err), "fdev_tree: bad arguments");
+        return 13;
+    }
+    if (n == 0) return 0;
+    int nremote = __builtin_popcount(remote_mask & ((1u << nsrc) - 1));
+    d->ctr.link_bytes += (double)n * (double)es * nremote;
+    d->ctr.hbm_bytes += (double)n * (double)es * (nsrc - nremote + 1);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (d->profiling) {
+        e0 = get_event(d);
+        e1 = get_event(d);
+        if (e0) (void)hipEventRecord(e0, d->stream);
+    }
+    // pieces of at most max_blocks vector workgroups (plan_tree refuses larger bodies)
+    const size_t piece = (size_t)d->max_blocks * 256 * (16 / es);
+    for (size_t off = 0; off < n; off += piece) {
+        ftar::TreeArgs A;
+        memset(&A, 0, sizeof(A));
+        for (int j = 0; j < nsrc; j++) A.src[j] = (const char *)src[j] + off * es;
+        A.out = (char *)out + off * es;
+        A.n = n - off < piece ? n - off : piece;
+        unsigned grid = ftar::plan_tree(&A, nsrc, es, d->max_blocks + 1);
+        if (grid == 0) {
+            snprintf(g_err, sizeof(g_err), "fdev_tree: plan failed");
+            return 13;
+        }
+        hipError_t e = ftar::launch_tree(dtype, op, nsrc, A, grid, d->stream);
+        if (e != hipSuccess) return set_err(e, "tree_kernel launch");
+    }
+    if (d->profiling && e0 && e1) {
+        (void)hipEventRecord(e1, d->stream);
+        d->pending.push_back(Pending{e0, e1, tag});
+    }
+    return 0;
+}
+
 int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     return run_on(d, d->stream, dtype, op, segs, nseg, tag);

@@ -79,6 +79,23 @@ struct SegIn {
     void *out2;
 };
 
+// Tree reduce: out[i] = balanced left-to-right tree of src[0..p-1][i] (p = 2, 4, 8, 16):
+// ((s0 op s1) op (s2 op s3)) op ...  With the sources in owner-relative order
+// (src[j] = vrank owner ^ j) this is exactly the value recursive halving leaves in the
+// owner's final block (every level: the owner's subtree first).
+constexpr int kMaxTree = 16;
+struct TreeArgs {
+    const void *src[kMaxTree];
+    void *out;
+    size_t n;      // elements
+    size_t head;   // scalar elements before the 16-byte vector body (co-aligned sources)
+    size_t nv;     // 16-byte vectors in the body (0 when the pointers are not co-aligned)
+    unsigned nvb;  // workgroups of the vector body; the rest do the scalar elements
+};
+// fills the alignment fields of A (src/out/n set) and returns the grid size
+unsigned plan_tree(TreeArgs *A, int p, size_t esize, unsigned max_blocks);
+hipError_t launch_tree(int dtype, int op, int p, const TreeArgs &A, unsigned grid, hipStream_t s);
+
 unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_blocks, KSegList *L);
 hipError_t launch_segments(int dtype, int op, const KSegList &L, unsigned grid, hipStream_t s);
 hipError_t launch_reduce_lds(int dtype, int op, void *inout, const void *in, size_t nvec, unsigned grid,

@@ -182,9 +182,104 @@ __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(uint4 *__restrict__ 
     }
 }
 
+// Tree reduce over p sources (one-hop reduce-scatter on the xGMI mesh): every lane loads
+// one 16-byte vector from each of the p sources -- p - 1 of them peers, so all links
+// stream at once -- and combines them in the schedule's tree.  Workgroups past the
+// vector body take the scalar head/tail (or everything, if the pointers are not
+// co-aligned), grid-stride.
+template <typename T, int OP, int P>
+__global__ __launch_bounds__(kBlock) void tree_kernel(TreeArgs A)
+{
+    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    if (b < A.nvb) {
+        const size_t i = (size_t)b * kBlock + threadIdx.x;
+        if (i >= A.nv) return;
+        uint4 v[P];
+#pragma unroll
+        for (int j = 0; j < P; j++) v[j] = ldnt((const uint4 *)((const T *)A.src[j] + A.head) + i);
+#pragma unroll
+        for (int w = 1; w < P; w <<= 1)
+#pragma unroll
+            for (int j = 0; j < P; j += 2 * w) v[j] = apply16<T, OP>(v[j], v[j + w]);
+        ((uint4 *)((T *)A.out + A.head))[i] = v[0];
+        return;
+    }
+    constexpr size_t E = 16 / sizeof(T);
+    const size_t tail0 = A.head + A.nv * E; // scalar elements: [0, head) and [tail0, n)
+    const size_t nscalar = A.head + (A.n - tail0);
+    const size_t stride = (size_t)(gridDim.x - A.nvb) * kBlock;
+    for (size_t k = (size_t)(b - A.nvb) * kBlock + threadIdx.x; k < nscalar; k += stride) {
+        const size_t e = k < A.head ? k : tail0 + (k - A.head);
+        T v[P];
+#pragma unroll
+        for (int j = 0; j < P; j++) v[j] = ((const T *)A.src[j])[e];
+#pragma unroll
+        for (int w = 1; w < P; w <<= 1)
+#pragma unroll
+            for (int j = 0; j < P; j += 2 * w) v[j] = apply<T, OP>(v[j], v[j + w]);
+        ((T *)A.out)[e] = v[0];
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------------
+unsigned plan_tree(TreeArgs *A, int p, size_t esize, unsigned max_blocks)
+{
+    uintptr_t mis = (uintptr_t)A->out & 15;
+    bool co = (16 % esize == 0) && (mis % esize == 0);
+    for (int j = 0; j < p; j++) co = co && (((uintptr_t)A->src[j] & 15) == mis);
+    A->head = A->nv = 0;
+    if (co) {
+        size_t head = mis ? (16 - mis) / esize : 0;
+        if (head > A->n) head = A->n;
+        A->head = head;
+        A->nv = (A->n - head) * esize / 16;
+    }
+    size_t nscalar = A->n - A->nv * (16 / esize);
+    size_t vb = (A->nv + kBlock - 1) / kBlock;
+    if (vb > max_blocks) return 0; // the caller splits larger blocks
+    size_t sb = (nscalar + kBlock - 1) / kBlock;
+    if (sb > 256) sb = 256;
+    A->nvb = (unsigned)vb;
+    return (unsigned)(vb + sb);
+}
+
+template <typename T, int OP>
+static hipError_t launch_tree_op(int p, const TreeArgs &A, unsigned grid, hipStream_t s)
+{
+    switch (p) {
+    case 2: hipLaunchKernelGGL((tree_kernel<T, OP, 2>), dim3(grid), dim3(kBlock), 0, s, A); break;
+    case 4: hipLaunchKernelGGL((tree_kernel<T, OP, 4>), dim3(grid), dim3(kBlock), 0, s, A); break;
+    case 8: hipLaunchKernelGGL((tree_kernel<T, OP, 8>), dim3(grid), dim3(kBlock), 0, s, A); break;
+    case 16: hipLaunchKernelGGL((tree_kernel<T, OP, 16>), dim3(grid), dim3(kBlock), 0, s, A); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_tree_t(int op, int p, const TreeArgs &A, unsigned grid, hipStream_t s)
+{
+    switch (op) {
+    case kSum: return launch_tree_op<T, kSum>(p, A, grid, s);
+    case kProd: return launch_tree_op<T, kProd>(p, A, grid, s);
+    case kMax: return launch_tree_op<T, kMax>(p, A, grid, s);
+    case kMin: return launch_tree_op<T, kMin>(p, A, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_tree(int dtype, int op, int p, const TreeArgs &A, unsigned grid, hipStream_t s)
+{
+    switch (dtype) {
+    case kInt32: return launch_tree_t<int32_t>(op, p, A, grid, s);
+    case kFloat32: return launch_tree_t<float>(op, p, A, grid, s);
+    case kInt64: return launch_tree_t<int64_t>(op, p, A, grid, s);
+    case kFloat64: return launch_tree_t<double>(op, p, A, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
 template <typename T>
 static hipError_t launch_t(int op, const KSegList &L, unsigned grid, hipStream_t s)
 {

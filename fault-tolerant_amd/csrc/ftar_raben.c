@@ -42,6 +42,7 @@ typedef struct {
     int bg_pending; /* step-0 redundancy copy still running on the background stream */
     int fast_io;    /* power of two, no recovery data: sbuf/rbuf used in place (see below) */
     int out_done;   /* the last allgather step already stored this rank's result in rbuf */
+    int mesh;       /* fast_io on the full mesh: one-hop reduce-scatter and allgather */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
 } rb_ctx;
 
@@ -245,6 +246,85 @@ static void rb_handler_ag(rb_ctx *x, uint64_t newf, int fs)
     c->stats.recoveries++;
 }
 
+/* The tolerant region at power-of-two p without an idle rank, on the full xGMI mesh.
+ *
+ * Recursive halving leaves in vrank v's final block the value
+ *     T(v, L),  T(v, 0) = x_v,  T(v, s+1) = T(v, s) op T(v ^ 2^s, s)
+ * (raben/rabenseifner.c:231-237: own window first, the partner's second; the partner's
+ * window was reduced by the same rule).  With the sources listed owner-relative
+ * (src[j] = x_{v^j}) that is the left-to-right balanced tree over j, which one tree
+ * kernel computes from p - 1 one-hop pulls -- every link of the GPU busy with 1/p of the
+ * vector instead of one link per step.  The allgather (:299-355) likewise pulls every
+ * peer's final block straight into rbuf.  Per rank and direction each link carries
+ * S/p for the reduce-scatter and S/p for the allgather: the mesh lower bound for an
+ * allreduce, half of what a 2-hop relay moves.
+ *
+ * The reference's per-step states are unobservable here: with no idle rank every
+ * handler aborts (new_entry = -1, raben/errhandler.c:207-211, 377-378), so a failure
+ * anywhere in a phase ends the job exactly as it would at that step's agree.  Every
+ * step's kill points are still passed (the injected death lands in the same phase), and
+ * each phase ends in the reference's agree + barrier. */
+static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
+{
+    ftar_comm *c = x->c;
+    const int L = x->steps, p = x->adjsize, v = x->vrank;
+    void *W = c->ws[WS_W];
+    int64_t own0 = x->rindex[L - 1], own_n = x->rcount[L - 1];
+
+    /* reduce-scatter: T(v, L) over this rank's final block */
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BEFORE);
+    const void *src[FDEV_MAX_TREE];
+    unsigned remote = 0;
+    for (int j = 0; j < p; j++) {
+        int u = v ^ j;
+        src[j] = j == 0 ? at(x, (void *)sbuf, own0) : at(x, ftar_buf(c, c->order[rb_real(x, u)], WS_IN), own0);
+        if (j) remote |= 1u << j;
+    }
+    double lb0 = ftar_link_bytes(c);
+    if (fdev_tree(c->dev, x->dtype, x->op, src, p, remote, at(x, W, own0), (size_t)own_n, FDEV_TAG_STEP0)) {
+        fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    ftar_drain(c);
+    c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
+    c->stats.steps += L;
+    c->stats.mesh_steps++;
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_AFTER);
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BARRIER);
+    uint64_t newf = ftar_step_sync(c, 2); /* agree + barrier (:258-265) */
+    if (newf) rb_handler_rs(x, newf, L - 1); /* no idle rank: aborts */
+
+    /* allgather: every peer's final block into rbuf, this rank's own out of W */
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
+    fdev_seg segs[FDEV_MAX_SEGS];
+    int ns = 0;
+    segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, own0), at(x, W, own0), NULL, (size_t)own_n, NULL};
+    for (int j = 1; j < p; j++) {
+        int u = v ^ j;
+        int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
+        rb_windows(u, x->count, L, ri, si, rc, sc);
+        void *PW = ftar_buf(c, c->order[rb_real(x, u)], WS_W);
+        segs[ns++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, rbuf, ri[L - 1]), at(x, PW, ri[L - 1]), NULL,
+                                (size_t)rc[L - 1], NULL};
+    }
+    ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
+    ftar_drain(c);
+    c->stats.steps += L;
+    c->stats.mesh_steps++;
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_AFTER);
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BARRIER);
+    newf = ftar_step_sync(c, 2); /* (:330-335) */
+    if (newf) rb_handler_ag(x, newf, 0); /* no idle rank: aborts */
+
+    /* ERRORS_ARE_FATAL barrier (:357-360); no post-step at rem = 0 */
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
+    ftar_sync_fatal(c);
+    ftar_stats_end(c);
+    return FTAR_SUCCESS;
+}
+
 int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar_dtype dtype, ftar_op op,
                                 ftar_comm *c)
 {
@@ -278,6 +358,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * half out of W in the same launch, and the prologue's three barriers (no pre-step
      * exchange at rem = 0) collapse into one.  Same operands, same bits. */
     x->fast_io = !x->keep_recov && x->rem == 0 && x->steps >= 1;
+    x->mesh = x->fast_io && c->mesh && c->size <= FDEV_MAX_TREE;
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);
@@ -287,7 +368,14 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     void *IN = c->ws[WS_IN], *W = c->ws[WS_W], *T = c->ws[WS_T];
     fdev_order_after(c->dev, c->user_stream); /* sbuf may still be in flight on the caller's stream */
     rb_vrank(x);
-    if (x->fast_io) { /* the half of sbuf peers pull at step 0 */
+    if (x->mesh) { /* every block of sbuf but this rank's own final one: the peers pull them */
+        rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+        int64_t b0 = x->rindex[x->steps - 1], b1 = b0 + x->rcount[x->steps - 1];
+        fdev_seg cp[2] = {{FDEV_COPY, 0, IN, sbuf, NULL, (size_t)b0, NULL},
+                          {FDEV_COPY, 0, at(x, IN, b1), at(x, (void *)sbuf, b1), NULL, (size_t)((int64_t)count - b1),
+                           NULL}};
+        ftar_run(c, x->dtype, x->op, cp, 2, FDEV_TAG_LOCAL);
+    } else if (x->fast_io) { /* the half of sbuf peers pull at step 0 */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         run_copy(x, at(x, IN, x->sindex[0]), at(x, (void *)sbuf, x->sindex[0]), x->scount[0], 0, FDEV_TAG_LOCAL);
     } else {
@@ -327,6 +415,8 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         ftar_sync_fatal(c); /* MPI_Barrier before the tolerant region (:166) */
     }
+
+    if (x->mesh) return rb_mesh(x, sbuf, rbuf);
 
     /* ---- reduce-scatter (:170-284) ---- */
     int step = 0;

@@ -162,7 +162,9 @@ typedef enum {
     FTAR_OPT_RELAY_MIN = 2,    /* smallest window, in bytes, that is relayed */
     FTAR_OPT_LOOP_SECONDS = 3, /* stretch of the step loop for fault-injection runs */
     FTAR_OPT_COPY_ENGINE = 4,  /* direct pulls as hipMemcpyAsync copies + local reduce (0/1) */
-    FTAR_OPT_REDUNDANCY = 5    /* Raben step-0 recovery copy: 0 only when a spare exists, 1 always */
+    FTAR_OPT_REDUNDANCY = 5,   /* Raben step-0 recovery copy: 0 only when a spare exists, 1 always */
+    FTAR_OPT_MESH = 6          /* Raben at power-of-two p without a spare: one-hop reduce-scatter and
+                                  allgather over the full mesh, same reduction tree (0/1) */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);
@@ -185,6 +187,7 @@ typedef struct {
     double drain_s;          /* host time spent waiting for the device stream */
     int    syncs;            /* agree/barrier rounds */
     int    relayed_steps;    /* exchange steps striped over 2-hop relays */
+    int    mesh_steps;       /* one-hop mesh exchanges (Raben reduce-scatter / allgather) */
 } ftar_stats;
 
 int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);

@@ -1,3 +1,4 @@
+import fcntl
 import importlib.util
 import os
 import subprocess
@@ -34,7 +35,10 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def hostsim():
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "hostsim")], check=True)
+    # one build at a time (pytest-xdist workers share the output directory)
+    with open(os.path.join(ROOT, "tests", "hostsim", ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "hostsim")], check=True)
     return os.path.join(ROOT, "tests", "hostsim", "_build")
 
 

@@ -148,3 +148,17 @@ def run_torch_worker(algo: str, inputs, devmap: str, env_extra: dict | None = No
         return ProbeRun(cp.returncode, cp.stdout, cp.stderr, outs, stats)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def with_specials(ins, seed):
+    """NaN, signed zeros and infinities at random places: MAX/MIN results then depend on
+    the operand order of every combination, so bit equality pins the reduction tree."""
+    rng = np.random.default_rng(seed)
+    sp = np.array([np.nan, -0.0, 0.0, np.inf, -np.inf], dtype=ins[0].dtype)
+    out = []
+    for x in ins:
+        x = x.copy()
+        idx = rng.choice(x.size, size=x.size // 8, replace=False)
+        x[idx] = rng.choice(sp, size=idx.size)
+        out.append(x)
+    return out

@@ -174,6 +174,40 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
     return 0;
 }
 
+#define TREE(T, UT)                                                                                         \
+    do {                                                                                                    \
+        for (size_t i = 0; i < n; i++) {                                                                    \
+            T v[16];                                                                                        \
+            for (int j = 0; j < nsrc; j++) v[j] = ((const T *)src[j])[i];                                   \
+            for (int w = 1; w < nsrc; w <<= 1)                                                              \
+                for (int j = 0; j < nsrc; j += 2 * w) {                                                     \
+                    T a = v[j], b = v[j + w];                                                               \
+                    switch (op) {                                                                           \
+                    case 0: v[j] = (T)((UT)a + (UT)b); break;                                               \
+                    case 1: v[j] = (T)((UT)a * (UT)b); break;                                               \
+                    case 2: v[j] = (a > b) ? a : b; break;                                                  \
+                    default: v[j] = (a < b) ? a : b; break;                                                 \
+                    }                                                                                       \
+                }                                                                                           \
+            ((T *)out)[i] = v[0];                                                                           \
+        }                                                                                                   \
+    } while (0)
+
+int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
+              size_t n, int tag)
+{
+    if (!(nsrc == 2 || nsrc == 4 || nsrc == 8 || nsrc == 16)) return 13;
+    switch (dtype) {
+    case 0: TREE(int32_t, uint32_t); break;
+    case 1: TREE(float, float); break;
+    case 2: TREE(int64_t, uint64_t); break;
+    default: TREE(double, double); break;
+    }
+    d->ctr.link_bytes += (double)n * (double)esz(dtype) * __builtin_popcount(remote_mask);
+    d->ctr.launches[tag]++;
+    return 0;
+}
+
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     return fdev_run(d, dtype, op, segs, nseg, tag);

@@ -76,8 +76,9 @@ int main(void)
         fclose(f);
         snprintf(path, sizeof(path), "%s/status_%d_%d.txt", dir, rank, it);
         f = fopen(path, "w");
-        fprintf(f, "%d %d %d %d %lld %lld %lld %d %d\n", rc, crank, csize, st.recoveries, (long long)(st.wall_s * 1e6),
-                (long long)(st.sync_wait_s * 1e6), (long long)(st.drain_s * 1e6), st.syncs, st.relayed_steps);
+        fprintf(f, "%d %d %d %d %lld %lld %lld %d %d %d\n", rc, crank, csize, st.recoveries,
+                (long long)(st.wall_s * 1e6), (long long)(st.sync_wait_s * 1e6), (long long)(st.drain_s * 1e6), st.syncs,
+                st.relayed_steps, st.mesh_steps);
         fclose(f);
     }
     ftar_finalize(comm);

@@ -114,7 +114,7 @@ def test_driver_checksums(oracle):
         assert "P: 4" in cp.stdout and "Size: 100000" in cp.stdout and "Time:" in cp.stdout
 
 
-RELAY_ALL = {"FTAR_RELAY_MIN": "0"}
+RELAY_ALL = {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}  # the step-by-step schedule, relayed
 
 
 @pytest.mark.parametrize("algo", ["raben", "rd"])
@@ -148,7 +148,7 @@ def test_large_windows_interleaved(oracle, algo, p, relay):
         assert min(st[0][8] for st in r.status.values()) > 0
 
 
-CE = {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"}
+CE = {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0", "FTAR_MESH": "0"}
 
 
 @pytest.mark.parametrize("algo", ["raben", "rd"])
@@ -190,3 +190,23 @@ def test_torch_device_buffers(oracle, algo, p, mode):
         for it in range(2):
             assert r.status[w][it] == (0, 1), (w, it, r.status[w][it])
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+
+
+@pytest.mark.parametrize("p,op,count", [(2, 0, 100003), (4, 0, 100003), (8, 0, 65536 + 5), (4, 2, 4099), (8, 3, 4099),
+                                        (4, 0, (1 << 22) + 13), (8, 1, (1 << 20) + 3)])
+def test_mesh_schedule(oracle, p, op, count):
+    """Power of two without a spare: one-hop reduce-scatter (tree kernel over p - 1
+    peer pulls) and allgather, bit-identical to the step-by-step schedule -- MAX/MIN with
+    NaN and signed zeros pin the operand order of every combination."""
+    dt = np.int32 if op == 1 else np.float32
+    ins = oracle.random_inputs(p, count, seed=p * 7 + op, dtype=dt)
+    if op >= 2:
+        ins = H.with_specials(ins, p + op)
+    o, r = _check(oracle.rabenseifner, "raben", ins, op=op)
+    assert all(st[0][9] == 2 for st in r.status.values()), r.status
+
+
+@pytest.mark.parametrize("kill", [(3, 1, 1, 2), (0, 2, 0, 1), (5, 1, 0, 0)])
+def test_mesh_kill_aborts(oracle, kill):
+    """Any death in the mesh phases ends the job like the reference at p = 8 (no idle rank)."""
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, 10007, seed=kill[0]), [kill])

@@ -175,7 +175,7 @@ def test_random_external_kill_never_wrong(hostsim, oracle, seed):
     subprocess.run(f"rm -f /dev/shm/ftarhs-ext{seed}-*", shell=True)
 
 
-RELAY_ALL = {"FTAR_RELAY_MIN": "0"}
+RELAY_ALL = {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}  # the step-by-step schedule, relayed
 
 
 @pytest.mark.parametrize("algo", ["raben", "rd"])
@@ -219,7 +219,7 @@ def test_relay_multi_kill_random(hostsim, oracle, seed):
     _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 2049, seed=seed), kills, env=RELAY_ALL)
 
 
-CE = {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"}
+CE = {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0", "FTAR_MESH": "0"}
 
 
 @pytest.mark.parametrize("algo", ["raben", "rd"])
@@ -290,7 +290,7 @@ def test_device_entry_points(hostsim, oracle, algo, p, mode, relay):
     power-of-two p Raben reads sbuf and writes rbuf in place (fast_io)."""
     env = dict(DEVICE_MODES[mode], FTAR_PROBE_DEVICE="1")
     if relay:
-        env["FTAR_RELAY_MIN"] = "0"
+        env.update(FTAR_RELAY_MIN="0", FTAR_MESH="0")
     ins = oracle.random_inputs(p, 1031, seed=p + 80)
     o = _fn(oracle, algo)(ins)
     r = H.run_probe(algo, ins, iters=2, backend="hostsim", env_extra=env)
@@ -299,3 +299,34 @@ def test_device_entry_points(hostsim, oracle, algo, p, mode, relay):
         for it in range(2):
             assert r.status[w][it][0] == 0, (w, it, r.status[w][it])
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+
+
+@pytest.mark.parametrize("p", [2, 4, 8, 16])
+@pytest.mark.parametrize("dtype,op", [(np.float32, 0), (np.int32, 0), (np.int64, 1), (np.float64, 2), (np.float32, 3)])
+def test_mesh_parity(hostsim, oracle, p, dtype, op):
+    """One-hop reduce-scatter + allgather (power of two, no spare): bit-identical to the
+    step-by-step schedule of the oracle for every op, NaN / signed-zero operand order
+    included."""
+    ins = oracle.random_inputs(p, 4099, seed=p * 10 + op, dtype=dtype)
+    if op >= 2:
+        ins = H.with_specials(ins, p + op)
+    o, r = _cmp(oracle.rabenseifner, "raben", ins, op=op)
+    assert all(st[0][9] == 2 for st in r.status.values()), r.status
+
+
+@pytest.mark.parametrize("p", [4, 8])
+def test_mesh_single_kill_sweep(hostsim, oracle, p):
+    """Every kill point of every step lands in the collapsed phases: the job aborts
+    exactly where the reference aborts (all of them, no idle rank)."""
+    ins = oracle.random_inputs(p, 1031, seed=p + 500)
+    n = 0
+    for v in range(p):
+        for ph in (0, 1, 2, 3):
+            for st in range(3):
+                for pt in range(3):
+                    ks = [(v, ph, st, pt)]
+                    if oracle.rabenseifner(ins, ks).status[v] != oracle.DEAD:
+                        continue
+                    _cmp(oracle.rabenseifner, "raben", ins, ks)
+                    n += 1
+    assert n > 0

@@ -8,6 +8,7 @@ report aborts the rank with a nonzero status, which fails the comparison below. 
 that die by injected SIGKILL or leave through MPI_Abort's _exit skip the leak check;
 every clean exit runs it.
 """
+import fcntl
 import os
 import subprocess
 
@@ -23,8 +24,11 @@ FLAGS = ("-O1 -g -std=c11 -Wall -Wno-unused-parameter -fPIC -D_GNU_SOURCE -fsani
 
 @pytest.fixture(scope="module")
 def asan_build():
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "hostsim"), "OUT=_build_asan", f"CFLAGS={FLAGS}",
-                    "all"], check=True)
+    # one build at a time (pytest-xdist workers share the output directory)
+    with open(os.path.join(ROOT, "tests", "hostsim", ".asan.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "hostsim"), "OUT=_build_asan",
+                        f"CFLAGS={FLAGS}", "all"], check=True)
     return H.HOSTSIM_ASAN
 
 
@@ -51,7 +55,8 @@ def test_asan_nofault(asan_build, oracle, algo, p):
     _run(oracle, algo, oracle.random_inputs(p, 1031, seed=p + 200), iters=2)
 
 
-@pytest.mark.parametrize("algo,p,env", [("raben", 8, {"FTAR_RELAY_MIN": "0"}), ("rd", 6, {"FTAR_RELAY_MIN": "0"}),
+@pytest.mark.parametrize("algo,p,env", [("raben", 8, {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}), ("raben", 8, {}),
+                                        ("rd", 6, {"FTAR_RELAY_MIN": "0"}),
                                         ("raben", 9, {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"}),
                                         ("raben", 4, {"FTAR_PROBE_DEVICE": "1", "FTAR_PROBE_INPLACE": "1",
                                                       "FTAR_PROBE_OFFSET": "3"})])
