@@ -263,7 +263,19 @@ def multi(args):
     cks_rd = int((yi.to(torch.int64) % 17).sum().item())
     cks_want = ((world * (world - 1) // 2) % 17) * args.count
     del xi, yi
+    # recursive doubling has no mesh form (it can recover at any p): relay or direct
+    rd_selection = None
+    relay_for_raben = comm.get_option(ftar.OPT_RELAY)
+    if world >= 3 and not args.no_variants:
+        comm.set_option(ftar.OPT_RELAY, 1)
+        t_r = quick(rd)
+        comm.set_option(ftar.OPT_RELAY, 0)
+        t_d = quick(rd)
+        comm.set_option(ftar.OPT_RELAY, 1 if t_r <= t_d else 0)
+        rd_selection = {"relay2hop_ms": round(t_r * 1e3, 4), "direct_ms": round(t_d * 1e3, 4),
+                        "chosen": "relay2hop" if t_r <= t_d else "direct"}
     t_rd, k_rd = timed(rd)
+    comm.set_option(ftar.OPT_RELAY, relay_for_raben)
     # the same schedules over plain pairwise exchanges (one link per step), with and
     # without the background-stream redundancy copy -- the reference's transport shape
     transports = {}
@@ -359,7 +371,7 @@ def multi(args):
                          "algorithmic_bytes_per_launch": step0_bytes, "kernel_ms": round(k_rb, 4)},
             "e2e_host_buffers": {"ms_per_step": round(t_e2e * 1e3, 3), "algbw_GBps": round(S / t_e2e / 1e9, 2)},
             "rd": {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
-                   "step0_kernel_ms": round(k_rd, 4)},
+                   "step0_kernel_ms": round(k_rd, 4), "transport_selection": rd_selection},
             "rccl_allreduce": ({"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2)}
                                if t_nc else None),
             "transport_selection": selection,
