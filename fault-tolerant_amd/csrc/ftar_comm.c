@@ -129,6 +129,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 0;
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
+    c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
     c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)4 << 20);
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
@@ -205,11 +206,62 @@ static void release_peers(ftar_comm *c)
             }
 }
 
+static void release_user_peers(ftar_comm *c)
+{
+    for (int w = 0; w < c->wsize; w++)
+        for (int k = 0; k < FTAR_UCACHE; k++)
+            if (c->ucache[w][k].base) {
+                fdev_unimport(c->dev, c->ucache[w][k].base);
+                c->ucache[w][k].base = NULL;
+                c->ucache[w][k].id = 0;
+            }
+}
+
+int ftar_publish_sbuf(ftar_comm *c, const void *sbuf, size_t bytes)
+{
+    ftar_slot *me = &c->job.shm->slot[c->wrank];
+    uint64_t id = 0;
+    size_t off = 0;
+    if (c->export_user && fdev_export_range(c->dev, sbuf, bytes, me->uhandle, &id, &off) == 0) {
+        me->uid = id;
+        me->uoff = off;
+        return 1;
+    }
+    me->uid = 0;
+    return 0;
+}
+
+void *ftar_peer_sbuf(ftar_comm *c, int w)
+{
+    ftar_slot *s = &c->job.shm->slot[w];
+    uint64_t id = s->uid;
+    if (!id) return NULL;
+    int victim = 0;
+    for (int k = 0; k < FTAR_UCACHE; k++) {
+        if (c->ucache[w][k].base && c->ucache[w][k].id == id) {
+            c->ucache[w][k].used = ++c->ucache_clock;
+            return (char *)c->ucache[w][k].base + s->uoff;
+        }
+        if (c->ucache[w][k].used < c->ucache[w][victim].used) victim = k;
+    }
+    if (c->ucache[w][victim].base) fdev_unimport(c->dev, c->ucache[w][victim].base);
+    void *base = NULL;
+    if (fdev_import(c->dev, s->uhandle, &base)) {
+        fprintf(stderr, "ftar: rank %d: cannot map rank %d's send buffer: %s\n", c->wrank, w, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    c->ucache[w][victim].id = id;
+    c->ucache[w][victim].base = base;
+    c->ucache[w][victim].used = ++c->ucache_clock;
+    return (char *)base + s->uoff;
+}
+
 int ftar_finalize(ftar_comm *c)
 {
     if (!c) return FTAR_ERR_ARG;
     ftar_sync_fatal(c);
     release_peers(c);
+    release_user_peers(c);
     ftar_sync_fatal(c); /* nobody maps our workspace any more */
     for (int b = 0; b < FTAR_NBUF; b++) fdev_free(c->dev, c->ws[b]);
     fdev_free(c->dev, c->hsend);

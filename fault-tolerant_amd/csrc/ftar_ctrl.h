@@ -48,6 +48,11 @@ typedef struct {
     /* per-round publication (RD: which buffer holds the accumulator), double-buffered by
      * round parity: written before arriving at round s into pubv[s % 2] tagged s */
     _Atomic uint64_t pubv[2];
+    /* the current call's send buffer, when the rank exports it instead of staging it in
+     * IN (written before the call's first barrier) */
+    unsigned char uhandle[FDEV_HANDLE_BYTES]; /* IPC handle of sbuf's allocation */
+    uint64_t uid;                             /* its allocation id; 0 = peers read IN */
+    uint64_t uoff;                            /* sbuf's byte offset in the allocation */
     char pad[64];
 } ftar_slot;
 

@@ -67,6 +67,10 @@ int fdev_device(const ftar_dev *d);
 int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle /* FDEV_HANDLE_BYTES */);
 int fdev_free(ftar_dev *d, void *ptr);
 int fdev_import(ftar_dev *d, const void *handle, void **ptr);
+/* Export the device allocation holding [ptr, ptr + bytes): its IPC handle, a per-process
+ * unique allocation id (a freed and re-used address gets a new one) and ptr's offset in
+ * it.  Nonzero if the memory cannot be shared (the caller then stages it). */
+int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, uint64_t *id, size_t *offset);
 int fdev_unimport(ftar_dev *d, void *ptr);
 
 /* Enqueue one segment kernel on the rank's stream. */

@@ -73,6 +73,8 @@ struct ftar_dev {
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
     fdev_counters ctr;
+    unsigned long long exp_id; // last exported user allocation (handle cached)
+    unsigned char exp_handle[FDEV_HANDLE_BYTES];
 };
 
 extern "C" {
@@ -98,6 +100,7 @@ int fdev_open(int device, ftar_dev **out)
     ftar_dev *d = new ftar_dev();
     d->device = device;
     d->profiling = 0;
+    d->exp_id = 0;
     memset(&d->ctr, 0, sizeof(d->ctr));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -179,6 +182,34 @@ int fdev_import(ftar_dev *d, const void *handle, void **ptr)
     hipIpcMemHandle_t h;
     memcpy(&h, handle, FDEV_HANDLE_BYTES);
     HIPCHK(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return 0;
+}
+
+int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, uint64_t *id, size_t *offset)
+{
+    HIPCHK(hipSetDevice(d->device));
+    unsigned long long bid = 0;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)ptr) != hipSuccess || bid == 0 ||
+        hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    size_t off = (size_t)((const char *)ptr - (const char *)base);
+    if (off + bytes > size) return 1;
+    if (d->exp_id != bid) {
+        hipIpcMemHandle_t h;
+        if (hipIpcGetMemHandle(&h, base) != hipSuccess) {
+            (void)hipGetLastError();
+            return 1;
+        }
+        memcpy(d->exp_handle, &h, FDEV_HANDLE_BYTES);
+        d->exp_id = bid;
+    }
+    memcpy(handle, d->exp_handle, FDEV_HANDLE_BYTES);
+    *id = bid;
+    *offset = off;
     return 0;
 }
 

@@ -48,6 +48,16 @@ struct ftar_comm {
 
     const void *uin; /* the current call's buffers (WS_UIN / WS_UOUT) */
     void *uout;
+    /* peers' exported send buffers (mesh Raben reads them in place): a few mappings per
+     * peer, keyed by the peer's allocation id */
+#define FTAR_UCACHE 4
+    struct {
+        uint64_t id;
+        void *base;
+        uint64_t used;
+    } ucache[FTAR_MAX_RANKS][FTAR_UCACHE];
+    uint64_t ucache_clock;
+    int export_user;     /* FTAR_EXPORT (default 1): let peers read sbuf in place where possible */
 
     /* host staging for the _host entry points */
     void *hsend, *hrecv;
@@ -77,6 +87,12 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes);
 void *ftar_buf(ftar_comm *c, int w, int b);
 /* this rank's buffer b: a workspace buffer or the call's WS_UIN / WS_UOUT */
 void *ftar_local(ftar_comm *c, int b);
+/* publish this call's sbuf for in-place peer reads (1) or report that peers must read
+ * the staged copy in IN (0); before the call's first barrier */
+int ftar_publish_sbuf(ftar_comm *c, const void *sbuf, size_t bytes);
+/* where original rank w's send buffer of this call is readable: its exported sbuf, or
+ * NULL if it staged it in IN; after the call's first barrier */
+void *ftar_peer_sbuf(ftar_comm *c, int w);
 
 /* agree over the survivors; returns newly failed original ranks (not yet acked) */
 uint64_t ftar_sync(ftar_comm *c);

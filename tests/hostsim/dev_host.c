@@ -137,6 +137,12 @@ int fdev_import(ftar_dev *d, const void *handle, void **ptr)
 
 int fdev_unimport(ftar_dev *d, void *ptr) { return drop(ptr, 0) == 0 ? 0 : 101; }
 
+/* caller memory here is private host memory: never shareable, the caller stages it */
+int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, uint64_t *id, size_t *offset)
+{
+    return 1;
+}
+
 #define LOOP(T, UT)                                                                                         \
     do {                                                                                                    \
         T *o = (T *)s->out;                                                                                 \

@@ -210,3 +210,9 @@ def test_mesh_schedule(oracle, p, op, count):
 def test_mesh_kill_aborts(oracle, kill):
     """Any death in the mesh phases ends the job like the reference at p = 8 (no idle rank)."""
     _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, 10007, seed=kill[0]), [kill])
+
+
+@pytest.mark.parametrize("p", [4, 8])
+def test_mesh_staged_sbuf(oracle, p):
+    """The mesh with sbuf staged in IN (FTAR_EXPORT=0) instead of read in place."""
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(p, 100003, seed=p + 600), env={"FTAR_EXPORT": "0"})
