@@ -216,3 +216,11 @@ def test_mesh_kill_aborts(oracle, kill):
 def test_mesh_staged_sbuf(oracle, p):
     """The mesh with sbuf staged in IN (FTAR_EXPORT=0) instead of read in place."""
     _check(oracle.rabenseifner, "raben", oracle.random_inputs(p, 100003, seed=p + 600), env={"FTAR_EXPORT": "0"})
+
+
+@pytest.mark.parametrize("algo,p", [("raben", 4), ("rd", 2)])
+def test_full_size_256MiB(oracle, algo, p):
+    """BASELINE's vector size (64 Mi float32 = 256 MiB per rank), bit-exact against the
+    oracle: the mesh / step schedules with full-size windows (capped grids, pieces)."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    _check(fn, algo, oracle.random_inputs(p, 1 << 26, seed=p + 700))
