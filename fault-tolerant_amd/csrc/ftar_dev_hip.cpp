@@ -107,11 +107,11 @@ int fdev_open(int device, ftar_dev **out)
     d->max_blocks = (unsigned)prop.multiProcessorCount * blocks_per_cu();
     if (d->max_blocks == 0) d->max_blocks = 2048;
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&d->bg, hipStreamNonBlocking));
+    d->bg = nullptr; // created on first use (ensure_bg): one hardware queue less per rank
     // default (fenced) events: recording one performs a system-scope sequentially
     // consistent fence -- L2 writeback and invalidation -- see sync_stream
     HIPCHK(hipEventCreateWithFlags(&d->fence_main, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&d->fence_bg, hipEventDisableTiming));
+    d->fence_bg = nullptr;
     // Peer access to every other GPU of the node: the exchanges read peers' HBM.
     for (int p = 0; p < ndev; p++) {
         if (p == device) continue;
@@ -130,16 +130,16 @@ void fdev_close(ftar_dev *d)
     if (!d) return;
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->stream);
-    (void)hipStreamSynchronize(d->bg);
+    if (d->bg) (void)hipStreamSynchronize(d->bg);
     for (auto &p : d->pending) {
         (void)hipEventDestroy(p.start);
         (void)hipEventDestroy(p.stop);
     }
     for (auto e : d->event_pool) (void)hipEventDestroy(e);
     (void)hipEventDestroy(d->fence_main);
-    (void)hipEventDestroy(d->fence_bg);
+    if (d->fence_bg) (void)hipEventDestroy(d->fence_bg);
     (void)hipStreamDestroy(d->stream);
-    (void)hipStreamDestroy(d->bg);
+    if (d->bg) (void)hipStreamDestroy(d->bg);
     delete d;
 }
 
@@ -218,6 +218,19 @@ int fdev_unimport(ftar_dev *d, void *ptr)
     if (!ptr) return 0;
     HIPCHK(hipSetDevice(d->device));
     HIPCHK(hipIpcCloseMemHandle(ptr));
+    return 0;
+}
+
+// The background stream exists only in ranks that use it (Raben's step-0 redundancy
+// copy with a spare): every stream is a hardware queue, and ranks that share a GPU (a
+// spare beside its partner, the one-GPU test box) time-slice once the device's queue
+// slots run out.
+static int ensure_bg(ftar_dev *d)
+{
+    if (d->bg) return 0;
+    HIPCHK(hipStreamCreateWithFlags(&d->bg, hipStreamNonBlocking));
+    // default (fenced) event: see sync_stream
+    HIPCHK(hipEventCreateWithFlags(&d->fence_bg, hipEventDisableTiming));
     return 0;
 }
 
@@ -324,6 +337,8 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
 
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
+    int rc = ensure_bg(d);
+    if (rc) return rc;
     hipEvent_t e = get_event(d);
     if (!e) return set_err(hipErrorOutOfMemory, "hipEventCreate");
     HIPCHK(hipEventRecord(e, d->stream));
@@ -338,6 +353,8 @@ int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int
     if (bytes == 0) return 0;
     hipStream_t st = d->stream;
     if (bg) { // ordered after the main stream, like fdev_run_bg
+        int rc = ensure_bg(d);
+        if (rc) return rc;
         hipEvent_t e = get_event(d);
         if (!e) return set_err(hipErrorOutOfMemory, "hipEventCreate");
         HIPCHK(hipEventRecord(e, d->stream));
@@ -410,6 +427,7 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 
 int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg)
 {
+    if (!d->bg) return harvest(d); // never used: nothing queued
     int rc = sync_stream(d, d->bg, poll, arg);
     if (rc) return rc;
     return harvest(d);
