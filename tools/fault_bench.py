@@ -7,6 +7,9 @@ Reports per-call wall time of rank 0 for the no-fault job and the fault job, and
 every survivor's result against the oracle.
 
 usage: python tools/fault_bench.py [count] [victim phase step point]
+FTAR_FB_RANKS=p changes the rank count (default 9).  More than 8 rank processes on the
+one GPU exceed its hardware contexts and get time-sliced (calls of 0.1-30 s); p = 5
+(4 + one idle spare) keeps the C5 structure within them.
 """
 import json
 import os
@@ -21,13 +24,16 @@ import harness as H  # noqa: E402
 import oracle as O  # noqa: E402
 
 
+NRANKS = int(os.environ.get("FTAR_FB_RANKS", "9"))
+
+
 def run(count, kill):
-    ins = O.random_inputs(9, count, seed=5)
+    ins = O.random_inputs(NRANKS, count, seed=5)
     kills = [kill + (1,)] if kill else []
-    r = H.run_probe("raben", ins, kills, iters=3, backend="gpu", devmap=",".join(["0"] * 9), timeout=600)
+    r = H.run_probe("raben", ins, kills, iters=3, backend="gpu", devmap=",".join(["0"] * NRANKS), timeout=600)
     o = O.rabenseifner(ins, [kill] if kill else [])
     ok = not r.aborted
-    for w in range(9):
+    for w in range(NRANKS):
         if o.status[w] == 0 and ok:
             ok &= np.array_equal(r.outputs[w][1].view(np.uint32), o.outputs[w].view(np.uint32))
     walls = [st[4] / 1e3 for st in r.status.get(0, [])]
@@ -40,7 +46,7 @@ def run(count, kill):
 def main():
     count = int(sys.argv[1]) if len(sys.argv) > 1 else (1 << 24)
     kill = tuple(int(v) for v in sys.argv[2:6]) if len(sys.argv) > 5 else (5, 1, 1, 0)
-    res = {"count": count, "bytes": count * 4, "nofault": run(count, None), "fault": run(count, kill)}
+    res = {"ranks": NRANKS, "count": count, "bytes": count * 4, "nofault": run(count, None), "fault": run(count, kill)}
     print(json.dumps(res))
 
 
