@@ -47,7 +47,9 @@ def cpu_model() -> str:
 def run(algo: str, p: int, count: int, dtype: str, reps: int) -> dict:
     exe = os.path.join(HS, OUT, "src", algo, "main")
     ftrun = os.path.join(HS, OUT, "bin", "ftrun")
-    env = dict(os.environ, FTAR_PIN_CPUS="1", FTAR_HOSTSIM_TAG=f"cpub{os.getpid()}", FTAR_DTYPE=dtype)
+    # the reference's shape: pairwise exchanges step by step (no relay, no mesh)
+    env = dict(os.environ, FTAR_PIN_CPUS="1", FTAR_HOSTSIM_TAG=f"cpub{os.getpid()}", FTAR_DTYPE=dtype,
+               FTAR_MESH="0", FTAR_RELAY="0")
     times, cpu = [], []
     for _ in range(reps):
         ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
@@ -80,7 +82,8 @@ def main():
     args = ap.parse_args()
     build()
     ncpu = len(os.sched_getaffinity(0))
-    res = {"kind": "port (product host C + host-memory device layer, one process per core)",
+    res = {"kind": "port (product host C + host-memory device layer, one process per core, pairwise step-by-step "
+                   "exchanges as in the reference)",
            "cpu_model": cpu_model(), "cpus": ncpu, "results": []}
     t0 = time.time()
     for algo in ("rd", "raben"):
