@@ -330,3 +330,12 @@ def test_mesh_single_kill_sweep(hostsim, oracle, p):
                     _cmp(oracle.rabenseifner, "raben", ins, ks)
                     n += 1
     assert n > 0
+
+
+@pytest.mark.parametrize("p", [2, 8, 16])
+@pytest.mark.parametrize("n", [1, 3, 17])
+def test_mesh_tiny_counts(hostsim, oracle, p, n):
+    """Vectors shorter than the rank count: empty final blocks on some ranks."""
+    o, r = _cmp(oracle.rabenseifner, "raben", oracle.random_inputs(p, n, seed=p + n),
+                env={"FTAR_PROBE_DEVICE": "1", "FTAR_PROBE_INPLACE": "1"})
+    assert all(st[0][9] == 2 for st in r.status.values())
