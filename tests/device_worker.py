@@ -5,8 +5,10 @@ input in a torch tensor on the rank's GPU (optionally at an element offset, opti
 in place: sbuf == rbuf), calls the device-pointer entry point twice and writes the
 results plus "rc sbuf_untouched" per call for tests/harness.run_torch_worker.
 
-env: FTAR_PROBE_DIR, FTAR_PROBE_ALGO=rd|raben, FTAR_PROBE_INPLACE, FTAR_PROBE_OFFSET
-(set by the harness), FTAR_RANK / FTAR_DEVICE (set by ftrun)
+env: FTAR_PROBE_DIR, FTAR_PROBE_ALGO=rd|raben, FTAR_PROBE_INPLACE, FTAR_PROBE_OFFSET,
+FTAR_PROBE_REALLOC=1 (the second call gets a freshly allocated sbuf holding -input, after
+the first one's memory went back to the driver: a re-used address must not be read
+through a stale peer mapping) (set by the harness), FTAR_RANK / FTAR_DEVICE (set by ftrun)
 """
 import importlib.util
 import os
@@ -24,6 +26,7 @@ def main():
     rank = int(os.environ["FTAR_RANK"])
     inplace = int(os.environ.get("FTAR_PROBE_INPLACE", "0"))
     off = int(os.environ.get("FTAR_PROBE_OFFSET", "0"))
+    realloc = int(os.environ.get("FTAR_PROBE_REALLOC", "0"))
     torch.cuda.set_device(int(os.environ.get("FTAR_DEVICE", "0")))
     spec = importlib.util.spec_from_file_location("ftar_amd", os.path.join(ROOT, "fault-tolerant_amd", "__init__.py"))
     ftar = importlib.util.module_from_spec(spec)
@@ -34,6 +37,12 @@ def main():
     want_in = torch.from_numpy(a)
     src = torch.zeros(n + off + 16, device="cuda")[off:off + n]
     for it in range(2):
+        if realloc and it:
+            del src
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            want_in = -want_in
+            src = torch.zeros(n + off + 16, device="cuda")[off:off + n]
         src.copy_(want_in)
         dst = src if inplace else torch.full((n + off + 16,), float("nan"), device="cuda")[off:off + n]
         fn = comm.allreduce_rabenseifner if algo == "raben" else comm.recursive_doubling

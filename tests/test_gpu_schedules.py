@@ -224,3 +224,17 @@ def test_full_size_256MiB(oracle, algo, p):
     oracle: the mesh / step schedules with full-size windows (capped grids, pieces)."""
     fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
     _check(fn, algo, oracle.random_inputs(p, 1 << 26, seed=p + 700))
+
+
+@pytest.mark.parametrize("p", [4, 8])
+def test_mesh_sbuf_reallocated(oracle, p):
+    """A freed and re-allocated send buffer (likely the same address, a new allocation)
+    is re-mapped by the peers: the second call (inputs negated) is exact."""
+    ins = oracle.random_inputs(p, 1 << 20, seed=p + 800)
+    o = oracle.rabenseifner(ins)
+    r = H.run_torch_worker("raben", ins, devmap=ALL_ON_GPU0, env_extra={"FTAR_PROBE_REALLOC": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    for w in range(p):
+        assert r.status[w][0] == (0, 1) and r.status[w][1] == (0, 1), r.status[w]
+        assert np.array_equal(r.outputs[w][0].view(np.uint32), o.outputs[w].view(np.uint32))
+        assert np.array_equal(r.outputs[w][1].view(np.uint32), (-o.outputs[w]).view(np.uint32))
