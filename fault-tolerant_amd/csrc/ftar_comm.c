@@ -217,25 +217,25 @@ static void release_user_peers(ftar_comm *c)
             }
 }
 
-int ftar_publish_sbuf(ftar_comm *c, const void *sbuf, size_t bytes)
+int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
 {
     ftar_slot *me = &c->job.shm->slot[c->wrank];
     uint64_t id = 0;
     size_t off = 0;
-    if (c->export_user && fdev_export_range(c->dev, sbuf, bytes, me->uhandle, &id, &off) == 0) {
-        me->uid = id;
-        me->uoff = off;
-        return 1;
-    }
-    me->uid = 0;
-    return 0;
+    ftar_inputs_done(c);
+    int ok = alias_ok && c->export_user && bytes && fdev_export_range(c->dev, sbuf, bytes, me->uhandle, &id, &off) == 0;
+    me->uid = ok ? id : 0;
+    me->uoff = off;
+    me->useq = (uint64_t)c->ncalls; /* a rank that dies before this point leaves an older tag */
+    if (ok) c->in_alias = sbuf;
+    return ok;
 }
 
-void *ftar_peer_sbuf(ftar_comm *c, int w)
+static void *peer_sbuf(ftar_comm *c, int w)
 {
     ftar_slot *s = &c->job.shm->slot[w];
     uint64_t id = s->uid;
-    if (!id) return NULL;
+    if (s->useq != (uint64_t)c->ncalls || !id) return NULL; /* staged in IN, or not published (dead) */
     int victim = 0;
     for (int k = 0; k < FTAR_UCACHE; k++) {
         if (c->ucache[w][k].base && c->ucache[w][k].id == id) {
@@ -247,6 +247,7 @@ void *ftar_peer_sbuf(ftar_comm *c, int w)
     if (c->ucache[w][victim].base) fdev_unimport(c->dev, c->ucache[w][victim].base);
     void *base = NULL;
     if (fdev_import(c->dev, s->uhandle, &base)) {
+        if (ftar_is_dead(c, w)) return NULL; /* its data is never used */
         fprintf(stderr, "ftar: rank %d: cannot map rank %d's send buffer: %s\n", c->wrank, w, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
@@ -254,6 +255,20 @@ void *ftar_peer_sbuf(ftar_comm *c, int w)
     c->ucache[w][victim].base = base;
     c->ucache[w][victim].used = ++c->ucache_clock;
     return (char *)base + s->uoff;
+}
+
+void ftar_resolve_inputs(ftar_comm *c)
+{
+    for (int i = 0; i < c->size; i++) {
+        int w = c->order[i];
+        if (w != c->wrank) c->peer_in[w] = peer_sbuf(c, w);
+    }
+}
+
+void ftar_inputs_done(ftar_comm *c)
+{
+    c->in_alias = NULL;
+    memset(c->peer_in, 0, sizeof(c->peer_in));
 }
 
 int ftar_finalize(ftar_comm *c)
@@ -468,13 +483,20 @@ void ftar_shrink(ftar_comm *c, uint64_t failed)
 
 /* ---- workspace ------------------------------------------------------------ */
 
-void *ftar_buf(ftar_comm *c, int w, int b) { return (w == c->wrank) ? c->ws[b] : c->peer[w][b]; }
+void *ftar_buf(ftar_comm *c, int w, int b)
+{
+    if (b == WS_IN) { /* this call's input may be the rank's own send buffer */
+        if (w == c->wrank) return c->in_alias ? (void *)c->in_alias : c->ws[WS_IN];
+        if (c->peer_in[w]) return c->peer_in[w];
+    }
+    return (w == c->wrank) ? c->ws[b] : c->peer[w][b];
+}
 
 void *ftar_local(ftar_comm *c, int b)
 {
     if (b == WS_UIN) return (void *)c->uin;
     if (b == WS_UOUT) return c->uout;
-    return c->ws[b];
+    return ftar_buf(c, c->wrank, b);
 }
 
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
@@ -543,6 +565,7 @@ void ftar_stats_end(ftar_comm *c)
     c->stats.hbm_bytes = k.hbm_bytes;
     c->stats.kernels = k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3] + k.launches[4];
     c->stats.comm_size_after = c->size;
+    ftar_inputs_done(c);
 }
 
 double ftar_link_bytes(ftar_comm *c)

@@ -53,6 +53,7 @@ typedef struct {
     unsigned char uhandle[FDEV_HANDLE_BYTES]; /* IPC handle of sbuf's allocation */
     uint64_t uid;                             /* its allocation id; 0 = peers read IN */
     uint64_t uoff;                            /* sbuf's byte offset in the allocation */
+    uint64_t useq;                            /* the call (1, 2, ...) these fields belong to */
     char pad[64];
 } ftar_slot;
 

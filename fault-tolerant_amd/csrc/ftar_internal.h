@@ -57,6 +57,10 @@ struct ftar_comm {
         uint64_t used;
     } ucache[FTAR_MAX_RANKS][FTAR_UCACHE];
     uint64_t ucache_clock;
+    /* this call's IN: the caller's exported sbuf itself (in_alias) or the staged copy;
+     * peer_in[w] likewise for every peer (NULL: its staged IN) -- see ftar_buf */
+    const void *in_alias;
+    void *peer_in[FTAR_MAX_RANKS];
     int export_user;     /* FTAR_EXPORT (default 1): let peers read sbuf in place where possible */
 
     /* host staging for the _host entry points */
@@ -87,12 +91,14 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes);
 void *ftar_buf(ftar_comm *c, int w, int b);
 /* this rank's buffer b: a workspace buffer or the call's WS_UIN / WS_UOUT */
 void *ftar_local(ftar_comm *c, int b);
-/* publish this call's sbuf for in-place peer reads (1) or report that peers must read
- * the staged copy in IN (0); before the call's first barrier */
-int ftar_publish_sbuf(ftar_comm *c, const void *sbuf, size_t bytes);
-/* where original rank w's send buffer of this call is readable: its exported sbuf, or
- * NULL if it staged it in IN; after the call's first barrier */
-void *ftar_peer_sbuf(ftar_comm *c, int w);
+/* Every call, before its first barrier: let IN be the caller's sbuf itself (exported to
+ * the peers, returns 1) when `alias_ok` and the memory can be shared, else publish that
+ * the peers read the staged copy the caller then makes (returns 0). */
+int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok);
+/* After the call's first barrier: map the peers' exported inputs (ftar_buf(w, WS_IN)). */
+void ftar_resolve_inputs(ftar_comm *c);
+/* End of a call: IN is the workspace buffer again everywhere. */
+void ftar_inputs_done(ftar_comm *c);
 
 /* agree over the survivors; returns newly failed original ranks (not yet acked) */
 uint64_t ftar_sync(ftar_comm *c);

@@ -277,9 +277,8 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
     unsigned remote = 0;
     for (int j = 0; j < p; j++) {
         int u = v ^ j;
-        int w = c->order[rb_real(x, u)];
-        void *pin = j ? ftar_peer_sbuf(c, w) : NULL; /* the peer's sbuf in place, or its staged IN */
-        src[j] = j == 0 ? at(x, (void *)sbuf, own0) : at(x, pin ? pin : ftar_buf(c, w, WS_IN), own0);
+        /* a peer's input: its sbuf in place, or its staged IN */
+        src[j] = j == 0 ? at(x, (void *)sbuf, own0) : at(x, ftar_buf(c, c->order[rb_real(x, u)], WS_IN), own0);
         if (j) remote |= 1u << j;
     }
     double lb0 = ftar_link_bytes(c);
@@ -370,15 +369,18 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     void *IN = c->ws[WS_IN], *W = c->ws[WS_W], *T = c->ws[WS_T];
     fdev_order_after(c->dev, c->user_stream); /* sbuf may still be in flight on the caller's stream */
     rb_vrank(x);
-    if (x->mesh) { /* peers pull every block of sbuf but this rank's own final one */
+    /* Where nothing writes IN (no pre-step, no recovery replay) the peers read sbuf in
+     * place; otherwise, or when its memory cannot be shared, it is staged in IN. */
+    int aliased = ftar_stage_input(c, sbuf, bytes, x->fast_io);
+    if (aliased) {
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
-        if (!ftar_publish_sbuf(c, sbuf, bytes)) { /* not shareable: stage it in IN */
-            int64_t b0 = x->rindex[x->steps - 1], b1 = b0 + x->rcount[x->steps - 1];
-            fdev_seg cp[2] = {{FDEV_COPY, 0, IN, sbuf, NULL, (size_t)b0, NULL},
-                              {FDEV_COPY, 0, at(x, IN, b1), at(x, (void *)sbuf, b1), NULL,
-                               (size_t)((int64_t)count - b1), NULL}};
-            ftar_run(c, x->dtype, x->op, cp, 2, FDEV_TAG_LOCAL);
-        }
+    } else if (x->mesh) { /* peers pull every block of sbuf but this rank's own final one */
+        rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+        int64_t b0 = x->rindex[x->steps - 1], b1 = b0 + x->rcount[x->steps - 1];
+        fdev_seg cp[2] = {{FDEV_COPY, 0, IN, sbuf, NULL, (size_t)b0, NULL},
+                          {FDEV_COPY, 0, at(x, IN, b1), at(x, (void *)sbuf, b1), NULL, (size_t)((int64_t)count - b1),
+                           NULL}};
+        ftar_run(c, x->dtype, x->op, cp, 2, FDEV_TAG_LOCAL);
     } else if (x->fast_io) { /* the half of sbuf peers pull at step 0 */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         run_copy(x, at(x, IN, x->sindex[0]), at(x, (void *)sbuf, x->sindex[0]), x->scount[0], 0, FDEV_TAG_LOCAL);
@@ -393,6 +395,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
         ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
         ftar_sync_fatal(c); /* every IN is ready; the barrier before the tolerant region (:166) */
+        ftar_resolve_inputs(c);
     } else {
         ftar_sync_fatal(c); /* every IN is ready */
         int64_t lh = (int64_t)count / 2, rh = (int64_t)count - lh;

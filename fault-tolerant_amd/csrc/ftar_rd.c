@@ -181,9 +181,15 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     ftar_stats_begin(c);
     int me = c->wrank;
 
-    ftar_ensure_workspace(c, count * x->es);
+    size_t bytes = count * x->es;
+    ftar_ensure_workspace(c, bytes);
     fdev_order_after(c->dev, c->user_stream);
-    run1(x, FDEV_COPY, c->ws[WS_IN], src, NULL, 0, FDEV_TAG_LOCAL);
+    /* Nothing writes IN after this: the peers read src in place when its memory can be
+     * shared -- unless it overlaps dst, which the last step writes while (with a single
+     * step) the partner may still be reading IN. */
+    const char *s0 = (const char *)src, *d0 = (const char *)dst;
+    int disjoint = s0 + bytes <= d0 || d0 + bytes <= s0;
+    if (!ftar_stage_input(c, src, bytes, disjoint)) run1(x, FDEV_COPY, c->ws[WS_IN], src, NULL, 0, FDEV_TAG_LOCAL);
     ftar_drain(c);
     x->cur = WS_IN;
     publish_cur(x);
@@ -201,10 +207,11 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BEFORE);
     uint64_t newf = ftar_sync(c); /* every IN is ready */
     if (newf & involved) ftar_abort(c, FTAR_ERR_PROC_FAILED);
+    ftar_resolve_inputs(c);
     int ia = index_of(x->active, x->nactive, me);
     if (ia >= 0 && ia < x->ninactive) {
         const void *P = ftar_buf(c, x->inactive[ia], WS_IN);
-        run1(x, FDEV_REDUCE, c->ws[WS_W], c->ws[WS_IN], P, FDEV_REMOTE_Y, FDEV_TAG_STEP); /* src = dst + src */
+        run1(x, FDEV_REDUCE, c->ws[WS_W], ftar_local(c, WS_IN), P, FDEV_REMOTE_Y, FDEV_TAG_STEP); /* src = dst + src */
         ftar_drain(c);
         x->cur = WS_W;
         publish_cur(x);
@@ -275,7 +282,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
         run1(x, FDEV_COPY, dst, ftar_buf(c, from, peer_cur(x, from)), NULL, FDEV_REMOTE_X, FDEV_TAG_STEP);
         c->stats.steps++;
     } else if (!dst_done) {
-        run1(x, FDEV_COPY, dst, c->ws[x->cur], NULL, 0, FDEV_TAG_LOCAL);
+        run1(x, FDEV_COPY, dst, ftar_local(c, x->cur), NULL, 0, FDEV_TAG_LOCAL);
     }
     ftar_drain(c);
     ftar_sync_fatal(c); /* main's MPI_Barrier (:134); peers are done reading */
