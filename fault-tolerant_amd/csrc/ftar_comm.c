@@ -228,6 +228,7 @@ int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
     me->uoff = off;
     me->useq = (uint64_t)c->ncalls; /* a rank that dies before this point leaves an older tag */
     if (ok) c->in_alias = sbuf;
+    if (c->verbose >= 2) fprintf(stderr, "ftar[%d] call %d: input %s\n", c->wrank, c->ncalls, ok ? "in place" : "staged");
     return ok;
 }
 

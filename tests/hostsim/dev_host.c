@@ -34,7 +34,9 @@ static struct {
     size_t n;
     char name[64];
     int own;
+    uint64_t id; /* allocation id (exportable allocations) */
 } g_map[MAXMAP];
+static uint64_t g_next_id;
 static int g_seq;
 static char g_err[256];
 
@@ -64,6 +66,7 @@ static int put_map(void *p, size_t n, const char *name, int own)
             g_map[i].p = p;
             g_map[i].n = n;
             g_map[i].own = own;
+            g_map[i].id = own ? ++g_next_id : 0;
             snprintf(g_map[i].name, sizeof(g_map[i].name), "%s", name);
             return 0;
         }
@@ -90,10 +93,12 @@ int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
     return 0;
 }
 
+/* "device" allocations of the library (the _host entry points' staging buffers) are
+ * shared-memory objects too, so they can be exported like hipMalloc memory */
 int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr)
 {
-    *ptr = malloc(bytes ? bytes : 1);
-    return *ptr ? 0 : 102;
+    unsigned char h[FDEV_HANDLE_BYTES];
+    return fdev_alloc_shared(d, bytes ? bytes : 1, ptr, h);
 }
 
 static int drop(void *ptr, int unlink_it)
@@ -137,9 +142,20 @@ int fdev_import(ftar_dev *d, const void *handle, void **ptr)
 
 int fdev_unimport(ftar_dev *d, void *ptr) { return drop(ptr, 0) == 0 ? 0 : 101; }
 
-/* caller memory here is private host memory: never shareable, the caller stages it */
+/* shareable when [ptr, ptr + bytes) lies in one of this process's shared-memory
+ * allocations; caller memory from malloc is not (the library then stages it) */
 int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, uint64_t *id, size_t *offset)
 {
+    const char *p = (const char *)ptr;
+    for (int i = 0; i < MAXMAP; i++) {
+        const char *b = (const char *)g_map[i].p;
+        if (!b || !g_map[i].own || p < b || p + bytes > b + g_map[i].n) continue;
+        memset(handle, 0, FDEV_HANDLE_BYTES);
+        snprintf((char *)handle, FDEV_HANDLE_BYTES, "%s", g_map[i].name);
+        *id = g_map[i].id;
+        *offset = (size_t)(p - b);
+        return 0;
+    }
     return 1;
 }
 
