@@ -161,7 +161,7 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
             }
             /* replay the dead rank's steps 0..fs (:106-200) into W's half this rank sent at
              * step 0 (= the dead rank's reduce window, unused here until the allgather) */
-            void *W = c->ws[WS_W], *IN = c->ws[WS_IN], *T = c->ws[WS_T];
+            void *W = c->ws[WS_W], *IN = ftar_local(c, WS_IN), *T = c->ws[WS_T];
             run_reduce(x, at(x, W, dri[0]), at(x, IN, dri[0]), at(x, T, dri[0]), drc[0], 0, FDEV_TAG_RECOV);
             for (int s = 1; s <= fs; s++) {
                 int pw = c->order[rb_real(x, vdead ^ (1 << s))];
@@ -369,10 +369,16 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     void *IN = c->ws[WS_IN], *W = c->ws[WS_W], *T = c->ws[WS_T];
     fdev_order_after(c->dev, c->user_stream); /* sbuf may still be in flight on the caller's stream */
     rb_vrank(x);
-    /* Where nothing writes IN (no pre-step, no recovery replay) the peers read sbuf in
-     * place; otherwise, or when its memory cannot be shared, it is staged in IN. */
-    int aliased = ftar_stage_input(c, sbuf, bytes, x->fast_io);
+    /* Where nothing writes this rank's IN -- every rank but the pre-step pairs; the
+     * handlers only read it -- the peers read sbuf in place; otherwise, or when its
+     * memory cannot be shared, it is staged in IN.  With a spare, the partner's step-0
+     * redundancy copy may still be reading sbuf while the last allgather step writes
+     * rbuf, so there sbuf and rbuf must not overlap. */
+    const char *s0 = (const char *)sbuf, *d0 = (const char *)rbuf;
+    int disjoint = s0 + bytes <= d0 || d0 + bytes <= s0;
+    int aliased = ftar_stage_input(c, sbuf, bytes, x->fast_io || (x->rank >= 2 * x->rem && disjoint));
     if (aliased) {
+        IN = (void *)sbuf;
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
     } else if (x->mesh) { /* peers pull every block of sbuf but this rank's own final one */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
@@ -398,6 +404,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         ftar_resolve_inputs(c);
     } else {
         ftar_sync_fatal(c); /* every IN is ready */
+        ftar_resolve_inputs(c);
         int64_t lh = (int64_t)count / 2, rh = (int64_t)count - lh;
         if (x->rank < 2 * x->rem) {
             if (x->rank % 2 != 0) { /* odd: reduce the right half with the even's right half */
