@@ -73,8 +73,11 @@ struct ftar_dev {
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
     fdev_counters ctr;
-    unsigned long long exp_id; // last exported user allocation (handle cached)
-    unsigned char exp_handle[FDEV_HANDLE_BYTES];
+    struct { // recently exported caller allocations (a handle per allocation id)
+        unsigned long long id, used;
+        unsigned char handle[FDEV_HANDLE_BYTES];
+    } exp[4];
+    unsigned long long exp_clock;
 };
 
 extern "C" {
@@ -100,7 +103,8 @@ int fdev_open(int device, ftar_dev **out)
     ftar_dev *d = new ftar_dev();
     d->device = device;
     d->profiling = 0;
-    d->exp_id = 0;
+    memset(d->exp, 0, sizeof(d->exp));
+    d->exp_clock = 0;
     memset(&d->ctr, 0, sizeof(d->ctr));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -198,16 +202,21 @@ int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, 
     }
     size_t off = (size_t)((const char *)ptr - (const char *)base);
     if (off + bytes > size) return 1;
-    if (d->exp_id != bid) {
+    int k = 0, victim = 0;
+    for (; k < 4 && d->exp[k].id != bid; k++)
+        if (d->exp[k].used < d->exp[victim].used) victim = k;
+    if (k == 4) {
         hipIpcMemHandle_t h;
         if (hipIpcGetMemHandle(&h, base) != hipSuccess) {
             (void)hipGetLastError();
             return 1;
         }
-        memcpy(d->exp_handle, &h, FDEV_HANDLE_BYTES);
-        d->exp_id = bid;
+        k = victim;
+        memcpy(d->exp[k].handle, &h, FDEV_HANDLE_BYTES);
+        d->exp[k].id = bid;
     }
-    memcpy(handle, d->exp_handle, FDEV_HANDLE_BYTES);
+    d->exp[k].used = ++d->exp_clock;
+    memcpy(handle, d->exp[k].handle, FDEV_HANDLE_BYTES);
     *id = bid;
     *offset = off;
     return 0;
