@@ -97,6 +97,15 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg);
 
 int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t bytes);
 int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t bytes);
+/* Host-buffer pipeline: chunk copies on their own streams (created on first use).
+ * fdev_h2d_async lands chunk `slot` (< FDEV_MAX_CHUNKS) and marks it with a fenced event;
+ * fdev_wait_h2d spins until it landed (visible to peers); fdev_d2h_async copies after
+ * everything queued on the rank's stream so far; fdev_sync_d2h waits for all of them. */
+#define FDEV_MAX_CHUNKS 16
+int fdev_h2d_async(ftar_dev *d, void *dst, const void *src, size_t bytes, int slot);
+int fdev_wait_h2d(ftar_dev *d, int slot, int (*poll)(void *), void *arg);
+int fdev_d2h_async(ftar_dev *d, void *dst, const void *src, size_t bytes);
+int fdev_sync_d2h(ftar_dev *d, int (*poll)(void *), void *arg);
 int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr);
 
 void fdev_profiling(ftar_dev *d, int on);

@@ -68,6 +68,8 @@ struct ftar_dev {
     hipStream_t bg;
     hipEvent_t fence_main; // fenced markers that sync_stream waits on
     hipEvent_t fence_bg;
+    hipStream_t h2d, d2h;  // host-buffer pipeline streams (created on first use)
+    hipEvent_t h2d_done[FDEV_MAX_CHUNKS], fence_d2h;
     int profiling;
     unsigned max_blocks;
     std::vector<Pending> pending;
@@ -116,6 +118,9 @@ int fdev_open(int device, ftar_dev **out)
     // consistent fence -- L2 writeback and invalidation -- see sync_stream
     HIPCHK(hipEventCreateWithFlags(&d->fence_main, hipEventDisableTiming));
     d->fence_bg = nullptr;
+    d->h2d = d->d2h = nullptr;
+    d->fence_d2h = nullptr;
+    memset(d->h2d_done, 0, sizeof(d->h2d_done));
     // Peer access to every other GPU of the node: the exchanges read peers' HBM.
     for (int p = 0; p < ndev; p++) {
         if (p == device) continue;
@@ -135,6 +140,8 @@ void fdev_close(ftar_dev *d)
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->stream);
     if (d->bg) (void)hipStreamSynchronize(d->bg);
+    if (d->h2d) (void)hipStreamSynchronize(d->h2d);
+    if (d->d2h) (void)hipStreamSynchronize(d->d2h);
     for (auto &p : d->pending) {
         (void)hipEventDestroy(p.start);
         (void)hipEventDestroy(p.stop);
@@ -144,6 +151,11 @@ void fdev_close(ftar_dev *d)
     if (d->fence_bg) (void)hipEventDestroy(d->fence_bg);
     (void)hipStreamDestroy(d->stream);
     if (d->bg) (void)hipStreamDestroy(d->bg);
+    for (int i = 0; i < FDEV_MAX_CHUNKS; i++)
+        if (d->h2d_done[i]) (void)hipEventDestroy(d->h2d_done[i]);
+    if (d->fence_d2h) (void)hipEventDestroy(d->fence_d2h);
+    if (d->h2d) (void)hipStreamDestroy(d->h2d);
+    if (d->d2h) (void)hipStreamDestroy(d->d2h);
     delete d;
 }
 
@@ -461,6 +473,66 @@ static int harvest(ftar_dev *d)
     }
     d->pending.swap(still);
     return 0;
+}
+
+static int ensure_pipe(ftar_dev *d)
+{
+    if (d->h2d) return 0;
+    HIPCHK(hipStreamCreateWithFlags(&d->h2d, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&d->d2h, hipStreamNonBlocking));
+    // default (fenced) events: a landed chunk is visible to the peers that pull it
+    for (int i = 0; i < FDEV_MAX_CHUNKS; i++) HIPCHK(hipEventCreateWithFlags(&d->h2d_done[i], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d->fence_d2h, hipEventDisableTiming));
+    return 0;
+}
+
+static int spin(hipEvent_t e, int (*poll)(void *), void *arg)
+{
+    for (;;) {
+        hipError_t r = hipEventQuery(e);
+        if (r == hipSuccess) return 0;
+        if (r != hipErrorNotReady) return set_err(r, "hipEventQuery");
+        if (poll) {
+            int rc = poll(arg);
+            if (rc) return rc;
+        }
+    }
+}
+
+int fdev_h2d_async(ftar_dev *d, void *dst, const void *src, size_t bytes, int slot)
+{
+    if (slot < 0 || slot >= FDEV_MAX_CHUNKS) return 13;
+    int rc = ensure_pipe(d);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d->h2d));
+    HIPCHK(hipEventRecord(d->h2d_done[slot], d->h2d));
+    return 0;
+}
+
+int fdev_wait_h2d(ftar_dev *d, int slot, int (*poll)(void *), void *arg)
+{
+    if (slot < 0 || slot >= FDEV_MAX_CHUNKS || !d->h2d) return 13;
+    return spin(d->h2d_done[slot], poll, arg);
+}
+
+int fdev_d2h_async(ftar_dev *d, void *dst, const void *src, size_t bytes)
+{
+    int rc = ensure_pipe(d);
+    if (rc) return rc;
+    hipEvent_t e = get_event(d);
+    if (!e) return set_err(hipErrorOutOfMemory, "hipEventCreate");
+    HIPCHK(hipEventRecord(e, d->stream));
+    HIPCHK(hipStreamWaitEvent(d->d2h, e, 0));
+    d->event_pool.push_back(e);
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, d->d2h));
+    return 0;
+}
+
+int fdev_sync_d2h(ftar_dev *d, int (*poll)(void *), void *arg)
+{
+    if (!d->d2h) return 0;
+    HIPCHK(hipEventRecord(d->fence_d2h, d->d2h));
+    return spin(d->fence_d2h, poll, arg);
 }
 
 int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t bytes)

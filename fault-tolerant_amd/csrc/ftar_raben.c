@@ -31,6 +31,11 @@
 #include <string.h>
 
 #define MAXSTEPS 32
+/* host-buffer pipeline: vectors of at least HOST_PIPE_MIN bytes go through in chunks of
+ * HOST_PIPE_CHUNK bytes (at most HOST_PIPE_MAX chunks, FDEV_MAX_CHUNKS) */
+#define HOST_PIPE_MIN ((size_t)16 << 20)
+#define HOST_PIPE_CHUNK ((size_t)8 << 20)
+#define HOST_PIPE_MAX 16
 
 typedef struct {
     ftar_comm *c;
@@ -555,9 +560,43 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
             return FTAR_ERR_NOMEM;
         c->hbytes = bytes;
     }
-    if (bytes && fdev_h2d(c->dev, c->hsend, sbuf, bytes)) return FTAR_ERR_DEVICE;
-    int rc = ftar_allreduce_rabenseifner(c->hsend, c->hrecv, count, dtype, op, c);
-    if (rc) return rc;
-    if (bytes && fdev_d2h(c->dev, rbuf, c->hrecv, bytes)) return FTAR_ERR_DEVICE;
+    /* Power of two without a spare (every failure aborts, so nothing is recovered across
+     * calls): the vector goes through as a pipeline of chunk Allreduces -- chunk k's
+     * H2D, chunk k-1's Allreduce and chunk k-2's D2H in flight at once (copy engines both
+     * ways, xGMI) -- instead of H2D, Allreduce, D2H in turn.  Each chunk is a complete
+     * fault-tolerant call (barriers, agree, abort). */
+    int p = c->size;
+    int nchunk = 1;
+    if (!c->redundancy && c->loop_seconds <= 0 && p >= 2 && (p & (p - 1)) == 0 &&
+        bytes >= HOST_PIPE_MIN) {
+        nchunk = (int)(bytes / HOST_PIPE_CHUNK);
+        if (nchunk > HOST_PIPE_MAX) nchunk = HOST_PIPE_MAX;
+    }
+    if (nchunk <= 1) {
+        if (bytes && fdev_h2d(c->dev, c->hsend, sbuf, bytes)) return FTAR_ERR_DEVICE;
+        int rc = ftar_allreduce_rabenseifner(c->hsend, c->hrecv, count, dtype, op, c);
+        if (rc) return rc;
+        if (bytes && fdev_d2h(c->dev, rbuf, c->hrecv, bytes)) return FTAR_ERR_DEVICE;
+        return FTAR_SUCCESS;
+    }
+    size_t per = (count + (size_t)nchunk - 1) / (size_t)nchunk;
+    per = (per + 63) / 64 * 64; /* chunk boundaries on 256-byte multiples */
+    int n = 0;
+    for (size_t off = 0; off < count; off += per, n++) {
+        size_t m = count - off < per ? count - off : per;
+        if (fdev_h2d_async(c->dev, (char *)c->hsend + off * es, (const char *)sbuf + off * es, m * es, n))
+            return FTAR_ERR_DEVICE;
+    }
+    n = 0;
+    for (size_t off = 0; off < count; off += per, n++) {
+        size_t m = count - off < per ? count - off : per;
+        if (fdev_wait_h2d(c->dev, n, ftar_ctrl_poll, &c->job)) return FTAR_ERR_DEVICE;
+        int rc = ftar_allreduce_rabenseifner((char *)c->hsend + off * es, (char *)c->hrecv + off * es, m, dtype, op,
+                                             c);
+        if (rc) return rc;
+        if (fdev_d2h_async(c->dev, (char *)rbuf + off * es, (char *)c->hrecv + off * es, m * es))
+            return FTAR_ERR_DEVICE;
+    }
+    if (fdev_sync_d2h(c->dev, ftar_ctrl_poll, &c->job)) return FTAR_ERR_DEVICE;
     return FTAR_SUCCESS;
 }

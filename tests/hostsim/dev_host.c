@@ -258,6 +258,18 @@ int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t n)
     memcpy(dst, src, n);
     return 0;
 }
+int fdev_h2d_async(ftar_dev *d, void *dst, const void *src, size_t n, int slot)
+{
+    memcpy(dst, src, n);
+    return 0;
+}
+int fdev_wait_h2d(ftar_dev *d, int slot, int (*poll)(void *), void *arg) { return poll ? poll(arg) : 0; }
+int fdev_d2h_async(ftar_dev *d, void *dst, const void *src, size_t n)
+{
+    memcpy(dst, src, n);
+    return 0;
+}
+int fdev_sync_d2h(ftar_dev *d, int (*poll)(void *), void *arg) { return poll ? poll(arg) : 0; }
 int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t n)
 {
     memcpy(dst, src, n);

@@ -238,3 +238,10 @@ def test_mesh_sbuf_reallocated(oracle, p):
         assert r.status[w][0] == (0, 1) and r.status[w][1] == (0, 1), r.status[w]
         assert np.array_equal(r.outputs[w][0].view(np.uint32), o.outputs[w].view(np.uint32))
         assert np.array_equal(r.outputs[w][1].view(np.uint32), (-o.outputs[w]).view(np.uint32))
+
+
+@pytest.mark.parametrize("p,count", [(8, (1 << 23) + 77), (2, (1 << 22) + 5)])
+def test_host_pipeline_chunks(oracle, p, count):
+    """Host-buffer entry point at >= 16 MiB, power of two: chunk Allreduces with H2D and
+    D2H on their own streams overlapping the exchanges, bit-exact to one call."""
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(p, count, seed=p + 900))

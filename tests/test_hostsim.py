@@ -339,3 +339,11 @@ def test_mesh_tiny_counts(hostsim, oracle, p, n):
     o, r = _cmp(oracle.rabenseifner, "raben", oracle.random_inputs(p, n, seed=p + n),
                 env={"FTAR_PROBE_DEVICE": "1", "FTAR_PROBE_INPLACE": "1"})
     assert all(st[0][9] == 2 for st in r.status.values())
+
+
+@pytest.mark.parametrize("p", [2, 4])
+@pytest.mark.parametrize("mesh", ["1", "0"])
+def test_host_pipeline_chunks(hostsim, oracle, p, mesh):
+    """Host buffers of >= 16 MiB at power-of-two p go through as a pipeline of chunk
+    Allreduces (H2D / Allreduce / D2H overlapped): same bits as one call."""
+    _cmp(oracle.rabenseifner, "raben", oracle.random_inputs(p, (1 << 22) + 77, seed=p + 900), env={"FTAR_MESH": mesh})
