@@ -130,6 +130,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
     c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
+    c->host_pipe = getenv("FTAR_HOST_PIPE") ? atoi(getenv("FTAR_HOST_PIPE")) : 1;
     c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)4 << 20);
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);

@@ -141,7 +141,6 @@ void fdev_close(ftar_dev *d)
     (void)hipStreamSynchronize(d->stream);
     if (d->bg) (void)hipStreamSynchronize(d->bg);
     if (d->h2d) (void)hipStreamSynchronize(d->h2d);
-    if (d->d2h) (void)hipStreamSynchronize(d->d2h);
     for (auto &p : d->pending) {
         (void)hipEventDestroy(p.start);
         (void)hipEventDestroy(p.stop);
@@ -155,7 +154,6 @@ void fdev_close(ftar_dev *d)
         if (d->h2d_done[i]) (void)hipEventDestroy(d->h2d_done[i]);
     if (d->fence_d2h) (void)hipEventDestroy(d->fence_d2h);
     if (d->h2d) (void)hipStreamDestroy(d->h2d);
-    if (d->d2h) (void)hipStreamDestroy(d->d2h);
     delete d;
 }
 
@@ -475,11 +473,17 @@ static int harvest(ftar_dev *d)
     return 0;
 }
 
+// The D2H copies ride on the background stream (idle in every call the pipeline runs
+// in: it only carries a spare's redundancy copy, joined before each call returns), so a
+// rank needs at most four streams -- null, main, background, H2D -- one hardware queue
+// each (GPU_MAX_HW_QUEUES = 4); a fifth would share a queue and serialize the copies.
 static int ensure_pipe(ftar_dev *d)
 {
     if (d->h2d) return 0;
+    int rc = ensure_bg(d);
+    if (rc) return rc;
     HIPCHK(hipStreamCreateWithFlags(&d->h2d, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&d->d2h, hipStreamNonBlocking));
+    d->d2h = d->bg;
     // default (fenced) events: a landed chunk is visible to the peers that pull it
     for (int i = 0; i < FDEV_MAX_CHUNKS; i++) HIPCHK(hipEventCreateWithFlags(&d->h2d_done[i], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&d->fence_d2h, hipEventDisableTiming));

@@ -62,6 +62,7 @@ struct ftar_comm {
     const void *in_alias;
     void *peer_in[FTAR_MAX_RANKS];
     int export_user;     /* FTAR_EXPORT (default 1): let peers read sbuf in place where possible */
+    int host_pipe;       /* FTAR_HOST_PIPE (default 1): chunk-pipelined host-buffer Raben where it applies */
 
     /* host staging for the _host entry points */
     void *hsend, *hrecv;

@@ -567,7 +567,7 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
      * fault-tolerant call (barriers, agree, abort). */
     int p = c->size;
     int nchunk = 1;
-    if (!c->redundancy && c->loop_seconds <= 0 && p >= 2 && (p & (p - 1)) == 0 &&
+    if (c->host_pipe && !c->redundancy && c->loop_seconds <= 0 && p >= 2 && (p & (p - 1)) == 0 &&
         bytes >= HOST_PIPE_MIN) {
         nchunk = (int)(bytes / HOST_PIPE_CHUNK);
         if (nchunk > HOST_PIPE_MAX) nchunk = HOST_PIPE_MAX;

@@ -56,6 +56,15 @@ if [[ $STEPS == *sweep* ]]; then
     rc=$?; tail -2 "$OUT/sweep_$n.log"; stop_on_fault $rc sweep_$n
   done
 fi
+if [[ $STEPS == *e2e* ]]; then
+  # host-buffer Raben end to end, chunk pipeline on / off, 1 / 2 ranks on GPU 0
+  for n in 2 4; do for hp in 1 0; do
+    FTAR_HOST_PIPE=$hp timeout -k 10 200 fault-tolerant_amd/bin/ftrun -np $n --devmap 0,0,0,0 python -u tools/e2e_probe.py \
+        >> "$OUT/e2e.json" 2>> "$OUT/e2e.err"
+    rc=$?; stop_on_fault $rc e2e_${n}_$hp
+  done; done
+  cat "$OUT/e2e.json"
+fi
 if [[ $STEPS == *syncprobe* ]]; then
   # device round trip of one step: kernel + marker event + host spin (tools/sync_probe.hip)
   timeout -k 10 120 tools/_build/sync_probe > "$OUT/sync_probe.json" 2>&1
