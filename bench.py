@@ -121,8 +121,10 @@ def single(args):
                                "1 MI355X", "count": args.count, "kernel_variant": args.variant,
                    "timing": args.timing},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("reduce_local_c2"),
-                     "kernel": "segment_kernel<float,SUM>", "algorithmic_bytes_per_launch": 3 * S,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic("reduce_local_c2_lds" if args.variant == 1 else "reduce_local_c2"),
+                     "kernel": "reduce_lds_kernel<float,SUM>" if args.variant == 1 else "segment_kernel<float,SUM>",
+                     "algorithmic_bytes_per_launch": 3 * S,
                      "kernel_ms": round(k_ms, 4)},
     }
     out["e2e"] = e2e_local(ftar, args.count)
@@ -391,7 +393,7 @@ def main():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--count", type=int, default=COUNT)
-    ap.add_argument("--variant", type=int, default=0, help="local-reduce kernel: 0 register, 1 LDS-DMA")
+    ap.add_argument("--variant", type=int, default=1, help="local-reduce kernel: 0 register, 1 LDS-DMA (default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing", choices=["region", "launch"], default="region",
                     help="N=1 kernel time: events around the timed region, or around every launch")

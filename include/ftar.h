@@ -148,7 +148,7 @@ int ftar_reduce_local(const void *in, void *inout, size_t count,
                       ftar_dtype dtype, ftar_op op, void *stream);
 
 /* Which implementation of the local-reduce kernel ftar_reduce_local launches:
- * 0 = register-streaming float4 kernel (default), 1 = LDS-DMA staged kernel. */
+ * 0 = register-streaming float4 kernel, 1 = LDS-DMA staged kernel (default). */
 int ftar_set_reduce_variant(int variant);
 
 /* Stream the comm orders its work after (hipStream_t, NULL = null stream). */

@@ -22,8 +22,8 @@ fi
 if [[ $STEPS == *bench* ]]; then
   timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
   rc=$?; cat "$OUT/bench.json"; stop_on_fault $rc bench
-  timeout -k 10 300 python bench.py --variant 1 --no-cpu-baseline > "$OUT/bench_v1.json" 2>> "$OUT/bench.err"
-  rc=$?; cat "$OUT/bench_v1.json"; stop_on_fault $rc bench_v1
+  timeout -k 10 300 python bench.py --variant 0 --no-cpu-baseline > "$OUT/bench_v0.json" 2>> "$OUT/bench.err"
+  rc=$?; cat "$OUT/bench_v0.json"; stop_on_fault $rc bench_v0
 fi
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
