@@ -229,11 +229,12 @@ int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
     me->uoff = off;
     me->useq = (uint64_t)c->ncalls; /* a rank that dies before this point leaves an older tag */
     if (ok) c->in_alias = sbuf;
+    c->in_bytes = bytes;
     if (c->verbose >= 2) fprintf(stderr, "ftar[%d] call %d: input %s\n", c->wrank, c->ncalls, ok ? "in place" : "staged");
     return ok;
 }
 
-static void *peer_sbuf(ftar_comm *c, int w)
+static void *peer_sbuf(ftar_comm *c, int w, int *failed)
 {
     ftar_slot *s = &c->job.shm->slot[w];
     uint64_t id = s->uid;
@@ -249,9 +250,8 @@ static void *peer_sbuf(ftar_comm *c, int w)
     if (c->ucache[w][victim].base) fdev_unimport(c->dev, c->ucache[w][victim].base);
     void *base = NULL;
     if (fdev_import(c->dev, s->uhandle, &base)) {
-        if (ftar_is_dead(c, w)) return NULL; /* its data is never used */
-        fprintf(stderr, "ftar: rank %d: cannot map rank %d's send buffer: %s\n", c->wrank, w, fdev_last_error());
-        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+        *failed = !ftar_is_dead(c, w); /* a dead rank's data is never used */
+        return NULL;
     }
     c->ucache[w][victim].id = id;
     c->ucache[w][victim].base = base;
@@ -259,11 +259,52 @@ static void *peer_sbuf(ftar_comm *c, int w)
     return (char *)base + s->uoff;
 }
 
+static uint64_t published_id(ftar_comm *c, int w)
+{
+    ftar_slot *s = &c->job.shm->slot[w];
+    return s->useq == (uint64_t)c->ncalls ? s->uid : 0;
+}
+
+/* Map the peers' exported inputs.  Every rank sees the same published ids, so when none
+ * changed since the last call every mapping is a cache hit everywhere; otherwise some
+ * rank may have to map a new allocation, and an extra agree round makes sure every rank
+ * managed before anyone reads through a mapping -- if one did not, the job stops
+ * exporting for good: the exporters stage their inputs in IN and the call goes on. */
 void ftar_resolve_inputs(ftar_comm *c)
 {
+    int changed = 0, failed = 0;
+    for (int i = 0; i < c->size; i++) { /* every member, this rank included: uniform */
+        int w = c->order[i];
+        if (published_id(c, w) != c->last_uid[w]) changed = 1;
+    }
     for (int i = 0; i < c->size; i++) {
         int w = c->order[i];
-        if (w != c->wrank) c->peer_in[w] = peer_sbuf(c, w);
+        if (w != c->wrank) c->peer_in[w] = peer_sbuf(c, w, &failed);
+    }
+    if (changed) {
+        ftar_slot *me = &c->job.shm->slot[c->wrank];
+        if (failed) {
+            fprintf(stderr, "ftar: rank %d: cannot map a peer's send buffer (%s): inputs are staged from now on\n",
+                    c->wrank, fdev_last_error());
+            me->ufail = (uint64_t)c->ncalls;
+        }
+        (void)ftar_sync(c); /* new failures are reported again by the schedule's next agree */
+        int any = 0;
+        for (int i = 0; i < c->size; i++) any |= c->job.shm->slot[c->order[i]].ufail == (uint64_t)c->ncalls;
+        if (any) {
+            c->export_user = 0;
+            if (c->in_alias) { /* stage the whole vector: what every schedule reads from IN */
+                fdev_seg s = {FDEV_COPY, 0, c->ws[WS_IN], c->in_alias, NULL, c->in_bytes / 4, NULL};
+                ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL);
+                ftar_drain(c);
+            }
+            ftar_inputs_done(c);
+            (void)ftar_sync(c); /* every staged copy is ready */
+        }
+    }
+    for (int i = 0; i < c->size; i++) {
+        int w = c->order[i];
+        c->last_uid[w] = c->export_user ? published_id(c, w) : 0;
     }
 }
 

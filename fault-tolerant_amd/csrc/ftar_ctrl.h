@@ -54,6 +54,7 @@ typedef struct {
     uint64_t uid;                             /* its allocation id; 0 = peers read IN */
     uint64_t uoff;                            /* sbuf's byte offset in the allocation */
     uint64_t useq;                            /* the call (1, 2, ...) these fields belong to */
+    uint64_t ufail;                           /* call in which this rank failed to map a peer's */
     char pad[64];
 } ftar_slot;
 

@@ -60,7 +60,9 @@ struct ftar_comm {
     /* this call's IN: the caller's exported sbuf itself (in_alias) or the staged copy;
      * peer_in[w] likewise for every peer (NULL: its staged IN) -- see ftar_buf */
     const void *in_alias;
+    size_t in_bytes;
     void *peer_in[FTAR_MAX_RANKS];
+    uint64_t last_uid[FTAR_MAX_RANKS]; /* peers' published allocation ids in the last call */
     int export_user;     /* FTAR_EXPORT (default 1): let peers read sbuf in place where possible */
     int host_pipe;       /* FTAR_HOST_PIPE (default 1): chunk-pipelined host-buffer Raben where it applies */
 

@@ -122,6 +122,14 @@ int fdev_free(ftar_dev *d, void *ptr)
 
 int fdev_import(ftar_dev *d, const void *handle, void **ptr)
 {
+    /* FTAR_HOSTSIM_FAIL_IMPORT=k: the k-th and later imports of this process fail (the
+     * workspace takes the first 4 (p - 1); later ones are peers' send buffers) */
+    static int nimport;
+    const char *fi = getenv("FTAR_HOSTSIM_FAIL_IMPORT");
+    if (fi && ++nimport >= atoi(fi)) {
+        snprintf(g_err, sizeof(g_err), "import refused (FTAR_HOSTSIM_FAIL_IMPORT)");
+        return 101;
+    }
     char name[FDEV_HANDLE_BYTES + 1];
     memcpy(name, handle, FDEV_HANDLE_BYTES);
     name[FDEV_HANDLE_BYTES] = 0;

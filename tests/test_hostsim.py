@@ -347,3 +347,19 @@ def test_host_pipeline_chunks(hostsim, oracle, p, mesh):
     """Host buffers of >= 16 MiB at power-of-two p go through as a pipeline of chunk
     Allreduces (H2D / Allreduce / D2H overlapped): same bits as one call."""
     _cmp(oracle.rabenseifner, "raben", oracle.random_inputs(p, (1 << 22) + 77, seed=p + 900), env={"FTAR_MESH": mesh})
+
+
+@pytest.mark.parametrize("algo,p", [("raben", 4), ("rd", 4), ("raben", 8), ("rd", 6)])
+def test_peer_input_map_failure_falls_back(hostsim, oracle, algo, p):
+    """A rank that cannot map a peer's exported send buffer: the extra agree round of the
+    call turns exporting off everywhere, the exporters stage their inputs, and the call
+    (and the next) are still exact."""
+    ins = oracle.random_inputs(p, 5003, seed=p + 950)
+    o = _fn(oracle, algo)(ins)
+    r = H.run_probe(algo, ins, iters=2, backend="hostsim",
+                    env_extra={"FTAR_HOSTSIM_FAIL_IMPORT": str(4 * (p - 1) + 1)})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "inputs are staged from now on" in r.stderr
+    for w in range(p):
+        for it in range(2):
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
