@@ -248,6 +248,8 @@ static void *peer_sbuf(ftar_comm *c, int w, int *failed)
         if (c->ucache[w][k].used < c->ucache[w][victim].used) victim = k;
     }
     if (c->ucache[w][victim].base) fdev_unimport(c->dev, c->ucache[w][victim].base);
+    c->ucache[w][victim].base = NULL;
+    c->ucache[w][victim].id = 0;
     void *base = NULL;
     if (fdev_import(c->dev, s->uhandle, &base)) {
         *failed = !ftar_is_dead(c, w); /* a dead rank's data is never used */
