@@ -547,6 +547,7 @@ void *ftar_local(ftar_comm *c, int b)
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
 {
     if (bytes <= c->ws_bytes && c->ws[0]) return FTAR_SUCCESS;
+    if (c->ws[0] && bytes < 2 * c->ws_bytes) bytes = 2 * c->ws_bytes; /* grow geometrically: few re-exports */
     size_t nb = (bytes + WS_ALIGN - 1) / WS_ALIGN * WS_ALIGN;
     if (nb == 0) nb = WS_ALIGN;
     ftar_sync_fatal(c); /* everybody is here */

@@ -159,20 +159,34 @@ void fdev_close(ftar_dev *d)
 
 int fdev_device(const ftar_dev *d) { return d->device; }
 
+// After memory has been exported and freed, a new hipMalloc of the same size can come
+// back at an address whose IPC export the runtime refuses (hipIpcGetMemHandle: invalid
+// argument; seen when the workspace grows mid-job).  Such a block is kept allocated
+// while the next one is tried, so the retry lands elsewhere, then all are freed.
 int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
 {
     HIPCHK(hipSetDevice(d->device));
-    void *p = nullptr;
-    HIPCHK(hipMalloc(&p, bytes));
-    hipIpcMemHandle_t h;
-    hipError_t e = hipIpcGetMemHandle(&h, p);
-    if (e != hipSuccess) {
-        (void)hipFree(p);
-        return set_err(e, "hipIpcGetMemHandle");
+    void *held[8];
+    int nheld = 0;
+    hipError_t e = hipSuccess;
+    for (;;) {
+        void *p = nullptr;
+        e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) break;
+        hipIpcMemHandle_t h;
+        e = hipIpcGetMemHandle(&h, p);
+        if (e == hipSuccess) {
+            memcpy(handle, &h, FDEV_HANDLE_BYTES);
+            *ptr = p;
+            for (int i = 0; i < nheld; i++) (void)hipFree(held[i]);
+            return 0;
+        }
+        (void)hipGetLastError();
+        held[nheld++] = p;
+        if (nheld == 8) break;
     }
-    memcpy(handle, &h, FDEV_HANDLE_BYTES);
-    *ptr = p;
-    return 0;
+    for (int i = 0; i < nheld; i++) (void)hipFree(held[i]);
+    return set_err(e, "hipMalloc + hipIpcGetMemHandle");
 }
 
 int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr)

@@ -245,3 +245,18 @@ def test_host_pipeline_chunks(oracle, p, count):
     """Host-buffer entry point at >= 16 MiB, power of two: chunk Allreduces with H2D and
     D2H on their own streams overlapping the exchanges, bit-exact to one call."""
     _check(oracle.rabenseifner, "raben", oracle.random_inputs(p, count, seed=p + 900))
+
+
+@pytest.mark.parametrize("p", [4, 8])
+def test_growing_sizes_one_job(tmp_path, p):
+    """Sizes 4 KiB .. 256 MiB in one job with fresh send buffers at every size: the
+    workspace grows and is re-exported while peers hold mappings of earlier buffers."""
+    import subprocess
+    import sys
+    env = dict(os.environ, FTAR_PROBE_DIR=str(tmp_path))
+    cmd = [os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ALL_ON_GPU0, sys.executable, "-u",
+           os.path.join(H.ROOT, "tests", "grow_worker.py")]
+    cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    for r in range(p):
+        assert (tmp_path / f"grow_{r}.txt").read_text() == "ok", (r, cp.stderr[-2000:])
