@@ -249,6 +249,7 @@ def multi(args):
     step0_bytes = timed.link_bytes
     relayed = comm.last_stats().relayed_steps > 0
     meshed = comm.last_stats().mesh_steps > 0
+    oneshot = comm.last_stats().mesh_steps == 1  # the mesh's one-launch form (p = 2, small vectors)
     # correctness spot check against torch.distributed's all_reduce on the same inputs
     # (fp32, different reduction order: |err| <= log2(p) * 2^-24 * sum|x_i|)
     ref = x.clone() if args.dist_backend == "nccl" else x.cpu()
@@ -335,7 +336,10 @@ def multi(args):
     classic = 2 * (1 - 2.0 ** -L) * S
     keep = world != r or comm.get_option(ftar.OPT_REDUNDANCY) != 0
     sched_bytes = ft_bytes if keep else classic
-    if meshed:
+    if oneshot:
+        # every peer's whole vector over its own link: S per link (= 2 S / p at p = 2)
+        t_roof = S / (XGMI_LINK_GBS * 1e9)
+    elif meshed:
         # one hop over p - 1 links: S/p per link for each of reduce-scatter and allgather
         t_roof = 2.0 * S / world / (XGMI_LINK_GBS * 1e9)
     elif relayed:
@@ -358,7 +362,7 @@ def multi(args):
                                    "rank, one rank per MI355X, pull exchanges over xGMI",
                        "count": args.count, "parallelism": f"{world} ranks"},
             "algbw_GBps": round(S / t_rb / 1e9, 2),
-            "transport": "mesh" if meshed else "relay2hop" if relayed else "direct",
+            "transport": "mesh-oneshot" if oneshot else "mesh" if meshed else "relay2hop" if relayed else "direct",
             "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "link_GBps": XGMI_LINK_GBS,
                                        "links_per_step": links, "t_roof_ms": round(t_roof * 1e3, 3),
                                        "frac": round(t_roof / t_rb, 4),
@@ -367,7 +371,9 @@ def multi(args):
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
                          "peak": peak, "unit": "GB/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
-                         "kernel": ("Raben mesh reduce-scatter: tree_kernel over p-1 one-hop pulls" if meshed
+                         "kernel": ("Raben one-shot mesh: tree_batch_kernel, every block in its owner's tree"
+                                    if oneshot
+                                    else "Raben mesh reduce-scatter: tree_kernel over p-1 one-hop pulls" if meshed
                                     else "Raben RS step 0, both relay phases (stripes pulled over r-1 links)" if relayed
                                     else "Raben RS step 0 reduce half (pull partner's half, reduce into W)"),
                          "algorithmic_bytes_per_launch": step0_bytes, "kernel_ms": round(k_rb, 4)},

@@ -129,6 +129,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 0;
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
+    c->oneshot_max = getenv("FTAR_ONESHOT_MAX") ? (size_t)atoll(getenv("FTAR_ONESHOT_MAX")) : ((size_t)1 << 20);
     c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
     c->host_pipe = getenv("FTAR_HOST_PIPE") ? atoi(getenv("FTAR_HOST_PIPE")) : 1;
     c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)4 << 20);
@@ -382,6 +383,7 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_COPY_ENGINE: c->copy_engine = v != 0; break;
     case FTAR_OPT_REDUNDANCY: c->redundancy = v != 0; break;
     case FTAR_OPT_MESH: c->mesh = v != 0; break;
+    case FTAR_OPT_ONESHOT_MAX: c->oneshot_max = (size_t)v; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;
@@ -398,6 +400,7 @@ int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
     case FTAR_OPT_COPY_ENGINE: *v = c->copy_engine; break;
     case FTAR_OPT_REDUNDANCY: *v = c->redundancy; break;
     case FTAR_OPT_MESH: *v = c->mesh; break;
+    case FTAR_OPT_ONESHOT_MAX: *v = (double)c->oneshot_max; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;

@@ -72,6 +72,10 @@ int fdev_import(ftar_dev *d, const void *handle, void **ptr);
  * it.  Nonzero if the memory cannot be shared (the caller then stages it). */
 int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, uint64_t *id, size_t *offset);
 int fdev_unimport(ftar_dev *d, void *ptr);
+/* 0 if the device can access [ptr, ptr + bytes): device memory inside one allocation,
+ * or pinned / managed memory; nonzero for pageable host memory or a range past the end
+ * of its allocation (the device entry points refuse those instead of faulting). */
+int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes);
 
 /* Enqueue one segment kernel on the rank's stream. */
 int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
@@ -81,6 +85,13 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
 #define FDEV_MAX_TREE 16
 int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
               size_t n, int tag);
+/* ntree (<= FDEV_MAX_BATCH) trees of nsrc (2, 4 or 8) sources in ONE launch: tree t
+ * reduces src[t * nsrc + j], j < nsrc, into out[t] over n[t] elements (remote_mask[t] as
+ * in fdev_tree).  Meant for small vectors: a tree beyond the device's workgroup budget
+ * makes it one launch per tree (same result). */
+#define FDEV_MAX_BATCH 8
+int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
+                    void *const *out, const size_t *n, int ntree, int tag);
 /* Enqueue on the rank's background stream, ordered after everything queued so far on
  * the main stream (it then overlaps later main-stream work). */
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);

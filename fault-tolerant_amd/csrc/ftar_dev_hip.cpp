@@ -80,6 +80,8 @@ struct ftar_dev {
         unsigned char handle[FDEV_HANDLE_BYTES];
     } exp[4];
     unsigned long long exp_clock;
+    struct { const void *ptr; size_t bytes; } checked[4]; // device-accessible ranges seen last
+    unsigned checked_next;
 };
 
 extern "C" {
@@ -107,6 +109,8 @@ int fdev_open(int device, ftar_dev **out)
     d->profiling = 0;
     memset(d->exp, 0, sizeof(d->exp));
     d->exp_clock = 0;
+    memset(d->checked, 0, sizeof(d->checked));
+    d->checked_next = 0;
     memset(&d->ctr, 0, sizeof(d->ctr));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -246,6 +250,32 @@ int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, 
     return 0;
 }
 
+int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes)
+{
+    for (auto &k : d->checked)
+        if (k.ptr == ptr && bytes <= k.bytes) return 0;
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    if (hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1; // not memory the runtime knows (pageable host memory)
+    }
+    if (a.type == hipMemoryTypeUnregistered) return 1;
+    if (a.type == hipMemoryTypeDevice) { // the whole range inside one allocation
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
+            (void)hipGetLastError();
+            return 1;
+        }
+        if ((size_t)((const char *)ptr - (const char *)base) + bytes > size) return 1;
+    }
+    d->checked[d->checked_next].ptr = ptr;
+    d->checked[d->checked_next].bytes = bytes;
+    d->checked_next = (d->checked_next + 1) % 4;
+    return 0;
+}
+
 int fdev_unimport(ftar_dev *d, void *ptr)
 {
     if (!ptr) return 0;
@@ -356,6 +386,55 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
         hipError_t e = ftar::launch_tree(dtype, op, nsrc, A, grid, d->stream);
         if (e != hipSuccess) return set_err(e, "tree_kernel launch");
     }
+    if (d->profiling && e0 && e1) {
+        (void)hipEventRecord(e1, d->stream);
+        d->pending.push_back(Pending{e0, e1, tag});
+    }
+    return 0;
+}
+
+int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
+                    void *const *out, const size_t *n, int ntree, int tag)
+{
+    size_t es = esize_of(dtype);
+    if (es == 0 || op < 0 || op > 3 || tag < 0 || tag >= FDEV_NTAGS || ntree < 1 || ntree > ftar::kMaxBatch ||
+        !(nsrc == 2 || nsrc == 4 || nsrc == 8)) {
+        snprintf(g_err, sizeof(g_err), "fdev_tree_batch: bad arguments");
+        return 13;
+    }
+    ftar::TreeBatch B;
+    memset(&B, 0, sizeof(B));
+    B.nt = 0;
+    double link = 0, hbm = 0;
+    for (int t = 0; t < ntree; t++) {
+        if (n[t] == 0) continue;
+        ftar::TreeArgs &A = B.t[B.nt++];
+        for (int j = 0; j < nsrc; j++) A.src[j] = src[t * nsrc + j];
+        A.out = out[t];
+        A.n = n[t];
+        int nremote = __builtin_popcount(remote_mask[t] & ((1u << nsrc) - 1));
+        link += (double)n[t] * (double)es * nremote;
+        hbm += (double)n[t] * (double)es * (nsrc - nremote + 1);
+    }
+    if (B.nt == 0) return 0;
+    unsigned grid = ftar::plan_tree_batch(&B, nsrc, es, d->max_blocks + 1);
+    if (grid == 0) { // a tree beyond the workgroup budget: one (split) launch per tree
+        for (int t = 0; t < ntree; t++) {
+            int rc = fdev_tree(d, dtype, op, src + (size_t)t * nsrc, nsrc, remote_mask[t], out[t], n[t], tag);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    d->ctr.link_bytes += link;
+    d->ctr.hbm_bytes += hbm;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (d->profiling) {
+        e0 = get_event(d);
+        e1 = get_event(d);
+        if (e0) (void)hipEventRecord(e0, d->stream);
+    }
+    hipError_t e = ftar::launch_tree_batch(dtype, op, nsrc, B, grid, d->stream);
+    if (e != hipSuccess) return set_err(e, "tree_batch_kernel launch");
     if (d->profiling && e0 && e1) {
         (void)hipEventRecord(e1, d->stream);
         d->pending.push_back(Pending{e0, e1, tag});

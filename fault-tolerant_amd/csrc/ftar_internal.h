@@ -81,6 +81,7 @@ struct ftar_comm {
     int copy_engine;     /* FTAR_COPY_ENGINE (default 0): direct pulls by hipMemcpyAsync */
     int redundancy;      /* FTAR_REDUNDANCY (default 0 = only when a spare can use it) */
     int mesh;            /* FTAR_MESH (default 1): one-hop Raben at power-of-two p without a spare */
+    size_t oneshot_max;  /* FTAR_ONESHOT_MAX bytes: mesh Raben in one launch up to this size */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
 };
 

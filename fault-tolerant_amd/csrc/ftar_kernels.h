@@ -95,6 +95,16 @@ struct TreeArgs {
 // fills the alignment fields of A (src/out/n set) and returns the grid size
 unsigned plan_tree(TreeArgs *A, int p, size_t esize, unsigned max_blocks);
 hipError_t launch_tree(int dtype, int op, int p, const TreeArgs &A, unsigned grid, hipStream_t s);
+// up to kMaxBatch trees of p <= kMaxBatchP sources in one launch; tree k owns
+// workgroups [first[k], first[k + 1])
+constexpr int kMaxBatch = 8, kMaxBatchP = 8;
+struct TreeBatch {
+    TreeArgs t[kMaxBatch];
+    unsigned first[kMaxBatch + 1];
+    int nt;
+};
+unsigned plan_tree_batch(TreeBatch *B, int p, size_t esize, unsigned max_blocks);
+hipError_t launch_tree_batch(int dtype, int op, int p, const TreeBatch &B, unsigned grid, hipStream_t s);
 
 unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_blocks, KSegList *L);
 hipError_t launch_segments(int dtype, int op, const KSegList &L, unsigned grid, hipStream_t s);

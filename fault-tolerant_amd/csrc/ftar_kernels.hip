@@ -188,9 +188,8 @@ __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(uint4 *__restrict__ 
 // vector body take the scalar head/tail (or everything, if the pointers are not
 // co-aligned), grid-stride.
 template <typename T, int OP, int P>
-__global__ __launch_bounds__(kBlock) void tree_kernel(TreeArgs A)
+__device__ __forceinline__ void tree_body(const TreeArgs &A, unsigned b, unsigned nblocks)
 {
-    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     if (b < A.nvb) {
         const size_t i = (size_t)b * kBlock + threadIdx.x;
         if (i >= A.nv) return;
@@ -207,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void tree_kernel(TreeArgs A)
     constexpr size_t E = 16 / sizeof(T);
     const size_t tail0 = A.head + A.nv * E; // scalar elements: [0, head) and [tail0, n)
     const size_t nscalar = A.head + (A.n - tail0);
-    const size_t stride = (size_t)(gridDim.x - A.nvb) * kBlock;
+    const size_t stride = (size_t)(nblocks - A.nvb) * kBlock;
     for (size_t k = (size_t)(b - A.nvb) * kBlock + threadIdx.x; k < nscalar; k += stride) {
         const size_t e = k < A.head ? k : tail0 + (k - A.head);
         T v[P];
@@ -219,6 +218,23 @@ __global__ __launch_bounds__(kBlock) void tree_kernel(TreeArgs A)
             for (int j = 0; j < P; j += 2 * w) v[j] = apply<T, OP>(v[j], v[j + w]);
         ((T *)A.out)[e] = v[0];
     }
+}
+
+template <typename T, int OP, int P>
+__global__ __launch_bounds__(kBlock) void tree_kernel(TreeArgs A)
+{
+    tree_body<T, OP, P>(A, (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x), gridDim.x);
+}
+
+// Several trees in one launch (the one-shot mesh Allreduce: every block of the vector,
+// each in its owner's tree): tree k takes workgroups [first[k], first[k + 1]).
+template <typename T, int OP, int P>
+__global__ __launch_bounds__(kBlock) void tree_batch_kernel(TreeBatch B)
+{
+    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    int k = 0;
+    while (k + 1 < B.nt && b >= B.first[k + 1]) k++;
+    tree_body<T, OP, P>(B.t[k], b - B.first[k], B.first[k + 1] - B.first[k]);
 }
 
 // ---------------------------------------------------------------------------------
@@ -280,6 +296,54 @@ hipError_t launch_tree(int dtype, int op, int p, const TreeArgs &A, unsigned gri
     default: return hipErrorInvalidValue;
     }
 }
+unsigned plan_tree_batch(TreeBatch *B, int p, size_t esize, unsigned max_blocks)
+{
+    unsigned total = 0;
+    for (int k = 0; k < B->nt; k++) {
+        B->first[k] = total;
+        unsigned g = plan_tree(&B->t[k], p, esize, max_blocks);
+        if (g == 0) return 0;
+        total += g;
+    }
+    B->first[B->nt] = total;
+    return total;
+}
+
+template <typename T, int OP>
+static hipError_t launch_batch_op(int p, const TreeBatch &B, unsigned grid, hipStream_t s)
+{
+    switch (p) {
+    case 2: hipLaunchKernelGGL((tree_batch_kernel<T, OP, 2>), dim3(grid), dim3(kBlock), 0, s, B); break;
+    case 4: hipLaunchKernelGGL((tree_batch_kernel<T, OP, 4>), dim3(grid), dim3(kBlock), 0, s, B); break;
+    case 8: hipLaunchKernelGGL((tree_batch_kernel<T, OP, 8>), dim3(grid), dim3(kBlock), 0, s, B); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_batch_t(int op, int p, const TreeBatch &B, unsigned grid, hipStream_t s)
+{
+    switch (op) {
+    case kSum: return launch_batch_op<T, kSum>(p, B, grid, s);
+    case kProd: return launch_batch_op<T, kProd>(p, B, grid, s);
+    case kMax: return launch_batch_op<T, kMax>(p, B, grid, s);
+    case kMin: return launch_batch_op<T, kMin>(p, B, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_tree_batch(int dtype, int op, int p, const TreeBatch &B, unsigned grid, hipStream_t s)
+{
+    switch (dtype) {
+    case kInt32: return launch_batch_t<int32_t>(op, p, B, grid, s);
+    case kFloat32: return launch_batch_t<float>(op, p, B, grid, s);
+    case kInt64: return launch_batch_t<int64_t>(op, p, B, grid, s);
+    case kFloat64: return launch_batch_t<double>(op, p, B, grid, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 template <typename T>
 static hipError_t launch_t(int op, const KSegList &L, unsigned grid, hipStream_t s)
 {

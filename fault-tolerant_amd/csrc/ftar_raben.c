@@ -48,6 +48,7 @@ typedef struct {
     int fast_io;    /* power of two, no recovery data: sbuf/rbuf used in place (see below) */
     int out_done;   /* the last allgather step already stored this rank's result in rbuf */
     int mesh;       /* fast_io on the full mesh: one-hop reduce-scatter and allgather */
+    int oneshot;    /* mesh of a small vector: every block in its owner's tree, one launch */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
 } rb_ctx;
 
@@ -331,6 +332,65 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
     return FTAR_SUCCESS;
 }
 
+/* One-shot mesh for small vectors: the allgather's data movement folded into the
+ * reduce-scatter launch.  Each rank evaluates EVERY block in its owner's tree,
+ * T(u, L) = tree over x_(u^j) (the same operands and order as rb_mesh's reduce-scatter,
+ * so the same bits), straight into rbuf: one launch instead of two, (p-1) S link bytes
+ * per rank instead of 2 (p-1) S / p -- cheaper below the size where a launch + drain
+ * (~11 us) outweighs the extra link time.  Kill points and the two agree rounds are
+ * rb_mesh's; with no idle rank a failure anywhere aborts. */
+static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
+{
+    ftar_comm *c = x->c;
+    const int L = x->steps, p = x->adjsize, v = x->vrank;
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BEFORE);
+    const void *src[FDEV_MAX_BATCH * FDEV_MAX_BATCH];
+    void *out[FDEV_MAX_BATCH];
+    size_t n[FDEV_MAX_BATCH];
+    unsigned remote[FDEV_MAX_BATCH];
+    for (int u = 0; u < p; u++) { /* block owned by vrank u */
+        int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
+        rb_windows(u, x->count, L, ri, si, rc, sc);
+        const int64_t off = ri[L - 1];
+        out[u] = at(x, rbuf, off);
+        n[u] = (size_t)rc[L - 1];
+        remote[u] = 0;
+        for (int j = 0; j < p; j++) {
+            const int w = u ^ j;
+            if (w == v) {
+                src[u * p + j] = at(x, (void *)sbuf, off);
+            } else {
+                src[u * p + j] = at(x, ftar_buf(c, c->order[rb_real(x, w)], WS_IN), off);
+                remote[u] |= 1u << j;
+            }
+        }
+    }
+    double lb0 = ftar_link_bytes(c);
+    if (fdev_tree_batch(c->dev, x->dtype, x->op, src, p, remote, out, n, p, FDEV_TAG_STEP0)) {
+        fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    ftar_drain(c);
+    c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
+    c->stats.steps += 2 * L;
+    c->stats.mesh_steps++;
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_AFTER);
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BARRIER);
+    uint64_t newf = ftar_step_sync(c, 2); /* agree + barrier (:258-265) */
+    if (newf) rb_handler_rs(x, newf, L - 1); /* no idle rank: aborts */
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_AFTER);
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BARRIER);
+    newf = ftar_step_sync(c, 2); /* (:330-335) */
+    if (newf) rb_handler_ag(x, newf, 0); /* no idle rank: aborts */
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
+    ftar_sync_fatal(c);
+    ftar_stats_end(c);
+    return FTAR_SUCCESS;
+}
+
 int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar_dtype dtype, ftar_op op,
                                 ftar_comm *c)
 {
@@ -348,6 +408,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     if (x->steps == -1) return FTAR_ERR_ARG;
     if (count == 0) return FTAR_ERR_UNKNOWN; /* copy_buffer(count <= 0), util.c:40-43 */
     if (count > (size_t)INT64_MAX / 16 || !sbuf || !rbuf) return FTAR_ERR_ARG;
+    /* device pointers: pageable host memory or a short allocation is refused, not faulted on */
+    if (fdev_check_ptr(c->dev, sbuf, count * x->es) || fdev_check_ptr(c->dev, rbuf, count * x->es))
+        return FTAR_ERR_ARG;
     x->adjsize = 1 << x->steps;
     x->rem = c->size - x->adjsize;
     /* The step-0 copy of the partner's other half (tmp, :191-197) is only ever read by
@@ -365,6 +428,12 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * exchange at rem = 0) collapse into one.  Same operands, same bits. */
     x->fast_io = !x->keep_recov && x->rem == 0 && x->steps >= 1;
     x->mesh = x->fast_io && c->mesh && c->size <= FDEV_MAX_TREE;
+    /* Uniform: count, p and the options are the same on every rank.  At p = 2 the
+     * one-shot form moves the same link bytes as the two-launch mesh (S per direction)
+     * in one launch, so it runs at every size; at p > 2 it reads (p - 2) S / p more per
+     * link and pays off only below oneshot_max. */
+    x->oneshot = x->mesh && c->size <= FDEV_MAX_BATCH && c->oneshot_max > 0 &&
+                 (c->size == 2 || count * (size_t)x->es <= c->oneshot_max);
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);
@@ -381,10 +450,16 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * rbuf, so there sbuf and rbuf must not overlap. */
     const char *s0 = (const char *)sbuf, *d0 = (const char *)rbuf;
     int disjoint = s0 + bytes <= d0 || d0 + bytes <= s0;
-    int aliased = ftar_stage_input(c, sbuf, bytes, x->fast_io || (x->rank >= 2 * x->rem && disjoint));
+    /* The one-shot launch writes rbuf while peers still read this rank's input: in place,
+     * that input must be staged (whole: peers read every block of it). */
+    int aliased = ftar_stage_input(c, sbuf, bytes,
+                                   x->oneshot ? disjoint : (x->fast_io || (x->rank >= 2 * x->rem && disjoint)));
     if (aliased) {
         IN = (void *)sbuf;
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+    } else if (x->oneshot) {
+        rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+        run_copy(x, IN, sbuf, (int64_t)count, 0, FDEV_TAG_LOCAL);
     } else if (x->mesh) { /* peers pull every block of sbuf but this rank's own final one */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         int64_t b0 = x->rindex[x->steps - 1], b1 = b0 + x->rcount[x->steps - 1];
@@ -435,6 +510,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         ftar_sync_fatal(c); /* MPI_Barrier before the tolerant region (:166) */
     }
 
+    if (x->oneshot) return rb_oneshot(x, sbuf, rbuf);
     if (x->mesh) return rb_mesh(x, sbuf, rbuf);
 
     /* ---- reduce-scatter (:170-284) ---- */

@@ -176,6 +176,9 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     if (x->es == 0 || op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
     if (count && (!src || !dst)) return FTAR_ERR_ARG;
     if (count == 0) return FTAR_SUCCESS;
+    /* device pointers: pageable host memory or a short allocation is refused, not faulted on */
+    if (fdev_check_ptr(c->dev, src, count * x->es) || fdev_check_ptr(c->dev, dst, count * x->es))
+        return FTAR_ERR_ARG;
     c->uin = src;
     c->uout = dst;
     ftar_stats_begin(c);

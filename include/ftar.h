@@ -119,6 +119,10 @@ int ftar_set_kills(ftar_comm *comm, const ftar_kill *kills, int nkills);
  * Device-resident, blocking (return when the result is in the output buffer).
  * `stream` ordering: the call first waits for all work queued on the stream set
  * with ftar_comm_set_stream (default: the null stream) to finish.
+ * Buffers must be device-accessible for count elements (device memory, or pinned /
+ * managed host memory): pageable host memory, or a range running past the end of its
+ * allocation, returns FTAR_ERR_ARG before anything is launched (use the _host entry
+ * points for host buffers).
  */
 
 /* Fault-tolerant Rabenseifner Allreduce (raben/rabenseifner.c:3-395).
@@ -163,8 +167,10 @@ typedef enum {
     FTAR_OPT_LOOP_SECONDS = 3, /* stretch of the step loop for fault-injection runs */
     FTAR_OPT_COPY_ENGINE = 4,  /* direct pulls as hipMemcpyAsync copies + local reduce (0/1) */
     FTAR_OPT_REDUNDANCY = 5,   /* Raben step-0 recovery copy: 0 only when a spare exists, 1 always */
-    FTAR_OPT_MESH = 6          /* Raben at power-of-two p without a spare: one-hop reduce-scatter and
+    FTAR_OPT_MESH = 6,         /* Raben at power-of-two p without a spare: one-hop reduce-scatter and
                                   allgather over the full mesh, same reduction tree (0/1) */
+    FTAR_OPT_ONESHOT_MAX = 7   /* mesh Raben up to this many bytes per vector (any size at p = 2): one
+                                  launch computes every block in its owner's tree into rbuf (0 = off) */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);

@@ -238,6 +238,21 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
     return 0;
 }
 
+int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes) { return ptr == NULL; }
+
+int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
+                    void *const *out, const size_t *n, int ntree, int tag)
+{
+    if (!(nsrc == 2 || nsrc == 4 || nsrc == 8) || ntree < 1 || ntree > FDEV_MAX_BATCH) return 13;
+    for (int t = 0; t < ntree; t++) {
+        int rc = fdev_tree(d, dtype, op, src + (size_t)t * nsrc, nsrc, remote_mask[t], out[t], n[t], tag);
+        if (rc) return rc;
+        d->ctr.launches[tag]--; /* one launch for the batch */
+    }
+    d->ctr.launches[tag]++;
+    return 0;
+}
+
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     return fdev_run(d, dtype, op, segs, nseg, tag);

@@ -9,8 +9,8 @@
  *
  * env: FTAR_PROBE_DIR, FTAR_PROBE_ALGO=rd|raben, FTAR_PROBE_DTYPE=0..3,
  *      FTAR_PROBE_OP=0..3, FTAR_PROBE_COUNT, FTAR_PROBE_ITERS (default 1),
- *      FTAR_PROBE_DEVICE=1 (device-pointer entry points on this process's own buffers:
- *      host-sim build only, where "device" memory is host memory),
+ *      FTAR_PROBE_DEVICE=1 (device-pointer entry points on this process's own malloc buffers:
+ *      host-sim: "device" memory is host memory; GPU build: must be refused),
  *      FTAR_PROBE_INPLACE=1 (send buffer = receive buffer),
  *      FTAR_PROBE_OFFSET=k (buffers start k elements past a 16-byte boundary)
  */

@@ -202,14 +202,52 @@ def test_mesh_schedule(oracle, p, op, count):
     ins = oracle.random_inputs(p, count, seed=p * 7 + op, dtype=dt)
     if op >= 2:
         ins = H.with_specials(ins, p + op)
-    o, r = _check(oracle.rabenseifner, "raben", ins, op=op)
+    o, r = _check(oracle.rabenseifner, "raben", ins, op=op, env={"FTAR_ONESHOT_MAX": "0"})
     assert all(st[0][9] == 2 for st in r.status.values()), r.status
 
 
+@pytest.mark.parametrize("p,op,count", [(2, 0, 100003), (4, 0, 4099), (8, 0, 65536 + 5), (4, 2, 4099), (8, 3, 4099),
+                                        (8, 1, 7)])
+def test_oneshot_schedule(oracle, p, op, count):
+    """Small vectors at power of two without a spare: one launch evaluates every block in
+    its owner's tree straight into rbuf, bit-identical to the step-by-step schedule --
+    MAX/MIN with NaN and signed zeros pin the operand order."""
+    dt = np.int32 if op == 1 else np.float32
+    ins = oracle.random_inputs(p, count, seed=p * 11 + op, dtype=dt)
+    if op >= 2:
+        ins = H.with_specials(ins, p + op)
+    o, r = _check(oracle.rabenseifner, "raben", ins, op=op, iters=2, env={"FTAR_ONESHOT_MAX": str(1 << 20)})
+    u = np.uint32
+    for w, st in r.status.items():
+        assert st[0][9] == 1 and st[1][9] == 1, (w, st)
+        assert np.array_equal(r.outputs[w][1].view(u), o.outputs[w].view(u)), w
+
+
+@pytest.mark.parametrize("p,count,mode", [(4, 4099, {}), (8, 65536 + 5, {"FTAR_PROBE_INPLACE": "1"}),
+                                          (8, 7, {"FTAR_PROBE_OFFSET": "3"}),
+                                          (8, (1 << 18) - 1, {"FTAR_PROBE_OFFSET": "1", "FTAR_PROBE_INPLACE": "1"}),
+                                          (4, 1000, {"FTAR_PROBE_REALLOC": "1"})])
+def test_oneshot_device_buffers(oracle, p, count, mode):
+    """The one-shot mesh on torch device buffers: peers read sbuf in place (staged when
+    sbuf == rbuf), misaligned offsets, a re-allocated sbuf; sbuf never written."""
+    ins = oracle.random_inputs(p, count, seed=p + count)
+    o = oracle.rabenseifner(ins)
+    r = H.run_torch_worker("raben", ins, devmap=ALL_ON_GPU0, env_extra=dict(mode, FTAR_ONESHOT_MAX=str(1 << 20)))
+    assert r.returncode == 0, r.stderr[-2000:]
+    sign = -1 if mode.get("FTAR_PROBE_REALLOC") else 1
+    for w in range(p):
+        assert r.status[w][0] == (0, 1) and r.status[w][1] == (0, 1), r.status[w]
+        assert np.array_equal(r.outputs[w][0].view(np.uint32), o.outputs[w].view(np.uint32))
+        assert np.array_equal(r.outputs[w][1].view(np.uint32), (sign * o.outputs[w]).view(np.uint32))
+
+
+@pytest.mark.parametrize("form", ["0", str(1 << 20)])
 @pytest.mark.parametrize("kill", [(3, 1, 1, 2), (0, 2, 0, 1), (5, 1, 0, 0)])
-def test_mesh_kill_aborts(oracle, kill):
-    """Any death in the mesh phases ends the job like the reference at p = 8 (no idle rank)."""
-    _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, 10007, seed=kill[0]), [kill])
+def test_mesh_kill_aborts(oracle, kill, form):
+    """Any death in the mesh phases (two-launch and one-shot) ends the job like the
+    reference at p = 8 (no idle rank)."""
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, 10007, seed=kill[0]), [kill],
+           env={"FTAR_ONESHOT_MAX": form})
 
 
 @pytest.mark.parametrize("p", [4, 8])
@@ -260,3 +298,16 @@ def test_growing_sizes_one_job(tmp_path, p):
     assert cp.returncode == 0, cp.stderr[-3000:]
     for r in range(p):
         assert (tmp_path / f"grow_{r}.txt").read_text() == "ok", (r, cp.stderr[-2000:])
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+def test_device_entry_refuses_pageable_host_memory(algo):
+    """Pageable host memory handed to the device entry points: FTAR_ERR_ARG on every rank
+    before anything is launched (no device fault), and the comm stays usable."""
+    rng = np.random.default_rng(5)
+    ins = [rng.standard_normal(1031).astype(np.float32) for _ in range(2)]
+    r = H.run_probe(algo, ins, iters=2, backend="gpu", devmap=ALL_ON_GPU0, timeout=120,
+                    env_extra={"FTAR_PROBE_DEVICE": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    for w in range(2):
+        assert r.status[w][0][0] == 13 and r.status[w][1][0] == 13, r.status[w]

@@ -301,24 +301,34 @@ def test_device_entry_points(hostsim, oracle, algo, p, mode, relay):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
+ONESHOT = {"mesh": "0", "oneshot": str(1 << 20)}  # FTAR_ONESHOT_MAX
+
+
+def _mesh_launches(p, form):
+    return 1 if form == "oneshot" and p <= 8 else 2  # FTAR_ONESHOT_MAX=0 turns the one-shot off at p = 2 too
+
+
+@pytest.mark.parametrize("form", sorted(ONESHOT))
 @pytest.mark.parametrize("p", [2, 4, 8, 16])
 @pytest.mark.parametrize("dtype,op", [(np.float32, 0), (np.int32, 0), (np.int64, 1), (np.float64, 2), (np.float32, 3)])
-def test_mesh_parity(hostsim, oracle, p, dtype, op):
-    """One-hop reduce-scatter + allgather (power of two, no spare): bit-identical to the
-    step-by-step schedule of the oracle for every op, NaN / signed-zero operand order
-    included."""
+def test_mesh_parity(hostsim, oracle, p, dtype, op, form):
+    """One-hop reduce-scatter + allgather (power of two, no spare), and its one-shot
+    form (every block in its owner's tree, one launch): bit-identical to the step-by-step
+    schedule of the oracle for every op, NaN / signed-zero operand order included."""
     ins = oracle.random_inputs(p, 4099, seed=p * 10 + op, dtype=dtype)
     if op >= 2:
         ins = H.with_specials(ins, p + op)
-    o, r = _cmp(oracle.rabenseifner, "raben", ins, op=op)
-    assert all(st[0][9] == 2 for st in r.status.values()), r.status
+    o, r = _cmp(oracle.rabenseifner, "raben", ins, op=op, env={"FTAR_ONESHOT_MAX": ONESHOT[form]})
+    assert all(st[0][9] == _mesh_launches(p, form) for st in r.status.values()), r.status
 
 
+@pytest.mark.parametrize("form", sorted(ONESHOT))
 @pytest.mark.parametrize("p", [4, 8])
-def test_mesh_single_kill_sweep(hostsim, oracle, p):
+def test_mesh_single_kill_sweep(hostsim, oracle, p, form):
     """Every kill point of every step lands in the collapsed phases: the job aborts
     exactly where the reference aborts (all of them, no idle rank)."""
     ins = oracle.random_inputs(p, 1031, seed=p + 500)
+    env = {"FTAR_ONESHOT_MAX": ONESHOT[form]}
     n = 0
     for v in range(p):
         for ph in (0, 1, 2, 3):
@@ -327,18 +337,39 @@ def test_mesh_single_kill_sweep(hostsim, oracle, p):
                     ks = [(v, ph, st, pt)]
                     if oracle.rabenseifner(ins, ks).status[v] != oracle.DEAD:
                         continue
-                    _cmp(oracle.rabenseifner, "raben", ins, ks)
+                    _cmp(oracle.rabenseifner, "raben", ins, ks, env=env)
                     n += 1
     assert n > 0
 
 
+@pytest.mark.parametrize("form", sorted(ONESHOT))
 @pytest.mark.parametrize("p", [2, 8, 16])
 @pytest.mark.parametrize("n", [1, 3, 17])
-def test_mesh_tiny_counts(hostsim, oracle, p, n):
-    """Vectors shorter than the rank count: empty final blocks on some ranks."""
+def test_mesh_tiny_counts(hostsim, oracle, p, n, form):
+    """Vectors shorter than the rank count: empty final blocks on some ranks (in place:
+    the one-shot form stages the input whole)."""
     o, r = _cmp(oracle.rabenseifner, "raben", oracle.random_inputs(p, n, seed=p + n),
-                env={"FTAR_PROBE_DEVICE": "1", "FTAR_PROBE_INPLACE": "1"})
-    assert all(st[0][9] == 2 for st in r.status.values())
+                env={"FTAR_PROBE_DEVICE": "1", "FTAR_PROBE_INPLACE": "1", "FTAR_ONESHOT_MAX": ONESHOT[form]})
+    assert all(st[0][9] == _mesh_launches(p, form) for st in r.status.values())
+
+
+@pytest.mark.parametrize("p", [2, 4, 8])
+@pytest.mark.parametrize("mode", sorted(DEVICE_MODES))
+def test_oneshot_device_buffers(hostsim, oracle, p, mode):
+    """One-shot mesh on the caller's device buffers (in place, misaligned), two calls:
+    exact, sbuf never written, one launch per call; above the threshold the two-launch
+    mesh runs."""
+    ins = oracle.random_inputs(p, 1031, seed=p + 960)
+    o = oracle.rabenseifner(ins)
+    for limit, launches in ((str(1 << 20), 1), ("1024", 1 if p == 2 else 2)):  # p = 2: one-shot at any size
+        env = dict(DEVICE_MODES[mode], FTAR_PROBE_DEVICE="1", FTAR_ONESHOT_MAX=limit)
+        r = H.run_probe("raben", ins, iters=2, backend="hostsim", env_extra=env)
+        assert r.returncode == 0, r.stderr[-1000:]
+        for w in range(p):
+            for it in range(2):
+                assert r.status[w][it][0] == 0, (w, it, r.status[w][it])
+                assert r.status[w][it][9] == launches, (limit, r.status[w][it])
+                assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
 @pytest.mark.parametrize("p", [2, 4])

@@ -8,7 +8,8 @@ Run as the ranks of one ftrun job (every rank on the GPU ftrun assigns it):
 Each size: 3 warm-up calls, then `reps` timed calls, each started right after an
 ftar_barrier; rank 0 reports the median of its per-call wall times (the ranks leave the
 barrier together, so this is one Allreduce from a common start).  Float32 SUM,
-uniform inputs.
+uniform inputs.  Up to 4 MiB (every size at 2 ranks) the two-launch mesh is timed too ("raben2", one-shot off),
+beside the default (one-shot up to FTAR_ONESHOT_MAX).
 """
 import importlib.util
 import json
@@ -36,7 +37,12 @@ def main():
         y = torch.empty_like(x)
         reps = 50 if n <= (1 << 20) else 10
         row = {"count": n, "bytes": 4 * n}
-        for name, fn in (("raben", comm.allreduce_rabenseifner), ("rd", comm.recursive_doubling)):
+        oneshot = comm.get_option(ftar.OPT_ONESHOT_MAX)
+        variants = [("raben", comm.allreduce_rabenseifner, oneshot), ("rd", comm.recursive_doubling, oneshot)]
+        if 4 * n <= (4 << 20) or int(os.environ["FTAR_SIZE"]) == 2:
+            variants.append(("raben2", comm.allreduce_rabenseifner, 0))
+        for name, fn, limit in variants:
+            comm.set_option(ftar.OPT_ONESHOT_MAX, limit)
             for _ in range(3):
                 assert fn(x, y) == 0
             ts = []
@@ -51,6 +57,8 @@ def main():
             row[name + "_syncs"] = st.syncs
             row[name + "_sync_wait_us"] = round(st.sync_wait_s * 1e6, 1)
             row[name + "_drain_us"] = round(st.drain_s * 1e6, 1)
+            row[name + "_launches"] = st.mesh_steps
+        comm.set_option(ftar.OPT_ONESHOT_MAX, oneshot)
         res.append(row)
         if rank == 0:
             print(json.dumps(row), flush=True)
