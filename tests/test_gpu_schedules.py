@@ -114,6 +114,28 @@ def test_driver_checksums(oracle):
         assert "P: 4" in cp.stdout and "Size: 100000" in cp.stdout and "Time:" in cp.stdout
 
 
+def _golden_checksums():
+    import csv
+    with open(os.path.join(H.ROOT, "tests", "golden", "ref_checksums.csv")) as f:
+        return {(r["algo"], int(r["NP"]), int(r["SIZE"])): int(r["RESULT"]) for r in csv.DictReader(f, delimiter=";")}
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [4, 6, 8])
+def test_driver_golden_checksums(algo, p):
+    """The drop-in drivers on the GPU against the reference's own recorded results
+    (data/data_compare rows committed in tests/golden/ref_checksums.csv): every rank's
+    printed checksum equals the reference's RESULT for that NP and SIZE -- the one-shot
+    mesh (small sizes), the two-launch mesh (4 MiB) and, at NP = 6, the pre-step path."""
+    gold = _golden_checksums()
+    for size in (1, 64, 16384, 1 << 20):
+        want = gold[(algo, p, size)]
+        cp, hello = H.run_driver(algo, p, size, backend="gpu", env_extra={"FTAR_DEVMAP": ALL_ON_GPU0})
+        assert cp.returncode == 0, (size, cp.stderr[-2000:])
+        assert sorted(hello) == list(range(p)), (size, cp.stdout[-1000:])
+        assert set(hello.values()) == {want}, (size, hello, want)
+
+
 RELAY_ALL = {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}  # the step-by-step schedule, relayed
 
 

@@ -115,6 +115,26 @@ def test_zero_count_returns_mpi_err_unknown(hostsim, oracle):
 
 
 @pytest.mark.parametrize("which", ["raben", "rd"])
+@pytest.mark.parametrize("n", [4, 6, 8, 12, 16])
+def test_drivers_match_golden_rows(hostsim, which, n):
+    """The drop-in drivers (host-sim device layer) against the reference's recorded
+    results: tests/golden/ref_checksums.csv rows for this NP (data/data_compare)."""
+    import csv
+    with open(os.path.join(H.ROOT, "tests", "golden", "ref_checksums.csv")) as f:
+        rows = [r for r in csv.DictReader(f, delimiter=";") if r["algo"] == which and int(r["NP"]) == n]
+    sizes = [int(r["SIZE"]) for r in rows]
+    assert sizes, "no golden rows"
+    for r in rows:
+        size = int(r["SIZE"])
+        if size not in (1, 3, 64, 16384, 65536) and size != max(sizes):
+            continue
+        cp, hello = H.run_driver(which, n, size)
+        assert cp.returncode == 0, cp.stderr
+        assert sorted(hello) == list(range(n))
+        assert set(hello.values()) == {int(r["RESULT"])}, (size, hello)
+
+
+@pytest.mark.parametrize("which", ["raben", "rd"])
 @pytest.mark.parametrize("n", [4, 5, 6, 8, 9])
 def test_drivers_print_reference_lines(hostsim, oracle, which, n):
     cp, hello = H.run_driver(which, n, 16384)
