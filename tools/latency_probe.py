@@ -1,0 +1,82 @@
+"""Where the fixed cost of a small Allreduce goes, ranks sharing one GPU (ftrun job):
+median per-call wall time, the part spent draining the stream, and the device time of
+the exchange kernel (hipEvents), next to a plain torch launch + synchronize issued by
+every rank at once (the device round trip without the library).
+
+    fault-tolerant_amd/bin/ftrun -np 2 --devmap 0,0 python tools/latency_probe.py [out.json]
+"""
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def med(v):
+    v = sorted(v)
+    return round(v[len(v) // 2] * 1e6, 1)
+
+
+def main():
+    rank = int(os.environ["FTAR_RANK"])
+    torch.cuda.set_device(int(os.environ.get("FTAR_DEVICE", "0")))
+    spec = importlib.util.spec_from_file_location("ftar_amd", os.path.join(ROOT, "fault-tolerant_amd", "__init__.py"))
+    ftar = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ftar)
+    comm = ftar.Comm.from_env()
+    x = torch.rand(1024, device="cuda")
+    y = torch.empty_like(x)
+    res = {"ranks": int(os.environ["FTAR_SIZE"])}
+    # plain device round trip, every rank at once
+    ts = []
+    for _ in range(200):
+        comm.barrier()
+        t0 = time.perf_counter()
+        y.copy_(x)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    res["torch_launch_sync_us"] = med(ts)
+    ts = []
+    for _ in range(200):
+        comm.barrier()
+        t0 = time.perf_counter()
+        comm.barrier()
+        ts.append(time.perf_counter() - t0)
+    res["ftar_barrier_us"] = med(ts)
+    for prof in (0, 1):
+        comm.set_profiling(bool(prof))
+        for name, fn, limit in (("raben_oneshot", comm.allreduce_rabenseifner, 1 << 20),
+                                ("raben_mesh", comm.allreduce_rabenseifner, 0), ("rd", comm.recursive_doubling, 0)):
+            comm.set_option(ftar.OPT_ONESHOT_MAX, limit)
+            for _ in range(5):
+                assert fn(x, y) == 0
+            wall, drain, sync, kern = [], [], [], []
+            for _ in range(200):
+                comm.barrier()
+                t0 = time.perf_counter()
+                assert fn(x, y) == 0
+                wall.append(time.perf_counter() - t0)
+                st = comm.last_stats()
+                drain.append(st.drain_s)
+                sync.append(st.sync_wait_s)
+                kern.append(st.step0_kernel_ms * 1e-3)
+            key = name + ("_profiled" if prof else "")
+            res[key] = {"wall_us": med(wall), "drain_us": med(drain), "sync_wait_us": med(sync)}
+            if prof:
+                res[key]["step0_kernel_us"] = med(kern)
+    comm.set_option(ftar.OPT_ONESHOT_MAX, 1 << 20)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+        if len(sys.argv) > 1:
+            with open(sys.argv[1], "w") as f:
+                json.dump(res, f)
+    comm.finalize()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
