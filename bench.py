@@ -304,6 +304,34 @@ def multi(args):
                 transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
         for o, v in defaults.items():
             comm.set_option(o, v)
+    # per-call time over message sizes on the node (max over ranks), with the chosen
+    # transport: the fixed cost per call and the one-shot threshold (FTAR_ONESHOT_MAX)
+    # measured one rank per GPU instead of estimated from the one-GPU rehearsals
+    sizes = {}
+    if not args.no_variants:
+        comm.set_profiling(False)  # no kernel events: the plain per-call cost
+        oneshot_max = comm.get_option(ftar.OPT_ONESHOT_MAX)
+        for n in (1 << 8, 1 << 14, 1 << 18, 1 << 20, 1 << 22):
+            if n > args.count:
+                continue
+            row = {"bytes": 4 * n}
+            for name, fn, extra in (("raben", comm.allreduce_rabenseifner, None),
+                                    ("raben_no_oneshot", comm.allreduce_rabenseifner, 0),
+                                    ("rd", comm.recursive_doubling, None)):
+                if extra is not None:
+                    if not (pow2 and comm.get_option(ftar.OPT_MESH) and oneshot_max > 0) or \
+                            (world > 2 and 4 * n > oneshot_max):
+                        continue
+                    comm.set_option(ftar.OPT_ONESHOT_MAX, extra)
+
+                def call(fn=fn, n=n):
+                    rc = fn(x, y, count=n)
+                    assert rc == 0, rc
+
+                row[name + "_us"] = round(quick(call, steps=20, warmup=3) * 1e6, 2)
+                comm.set_option(ftar.OPT_ONESHOT_MAX, oneshot_max)
+            sizes[str(4 * n)] = row
+        comm.set_profiling(True)
     # end-to-end with host buffers: pinned H2D + device Allreduce + D2H (never the value)
     xh = x.cpu().pin_memory()
     yh = torch.empty_like(xh).pin_memory()
@@ -384,6 +412,7 @@ def multi(args):
                                if t_nc else None),
             "transport_selection": selection,
             "transports": transports,
+            "size_sweep_us": sizes,
             "max_abs_err_vs_rccl": err,
             "int32_rank_checksum_ok": {"raben": cks_raben == cks_want, "rd": cks_rd == cks_want},
             "cpu_baseline": None,
