@@ -640,10 +640,15 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
      * calls): the vector goes through as a pipeline of chunk Allreduces -- chunk k's
      * H2D, chunk k-1's Allreduce and chunk k-2's D2H in flight at once (copy engines both
      * ways, xGMI) -- instead of H2D, Allreduce, D2H in turn.  Each chunk is a complete
-     * fault-tolerant call (barriers, agree, abort). */
+     * fault-tolerant call (barriers, agree, abort).
+     * Chunks move the block boundaries, and an element's tree takes its operands in its
+     * owner's order (src[j] = x_(owner ^ j)): the unordered tree is the same for every
+     * owner, so the bits are too wherever the op commutes exactly -- integers, float
+     * SUM/PROD -- but not float MAX/MIN (NaN, signed zeros), which stay one call. */
     int p = c->size;
     int nchunk = 1;
-    if (c->host_pipe && !c->redundancy && c->loop_seconds <= 0 && p >= 2 && (p & (p - 1)) == 0 &&
+    int commutes = dtype == FTAR_INT32 || dtype == FTAR_INT64 || op == FTAR_SUM || op == FTAR_PROD;
+    if (c->host_pipe && commutes && !c->redundancy && c->loop_seconds <= 0 && p >= 2 && (p & (p - 1)) == 0 &&
         bytes >= HOST_PIPE_MIN) {
         nchunk = (int)(bytes / HOST_PIPE_CHUNK);
         if (nchunk > HOST_PIPE_MAX) nchunk = HOST_PIPE_MAX;

@@ -307,6 +307,20 @@ def test_host_pipeline_chunks(oracle, p, count):
     _check(oracle.rabenseifner, "raben", oracle.random_inputs(p, count, seed=p + 900))
 
 
+@pytest.mark.parametrize("op", [2, 3])
+def test_host_pipeline_operand_order(oracle, op):
+    """Float MAX/MIN host calls >= 16 MiB stay one call (a chunk pipeline would move block
+    owners and with them the operand order): NaN and signed zeros bit-exact."""
+    p = 4
+    ins = oracle.random_inputs(p, (1 << 22) + 77, seed=p + 40 * op)
+    rng = np.random.default_rng(p + op)
+    for x in ins:
+        k = rng.integers(0, x.size, 1 << 16)
+        x[k[: 1 << 15]] = np.nan
+        x[k[1 << 15:]] = rng.choice(np.array([0.0, -0.0], dtype=np.float32), 1 << 15)
+    _check(oracle.rabenseifner, "raben", ins, op=op)
+
+
 @pytest.mark.parametrize("p", [4, 8])
 def test_growing_sizes_one_job(tmp_path, p):
     """Sizes 4 KiB .. 256 MiB in one job with fresh send buffers at every size: the

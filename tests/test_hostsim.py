@@ -414,3 +414,18 @@ def test_peer_input_map_failure_falls_back(hostsim, oracle, algo, p):
     for w in range(p):
         for it in range(2):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+
+
+@pytest.mark.parametrize("p", [2, 4])
+@pytest.mark.parametrize("op", [2, 3])
+def test_host_pipeline_operand_order(hostsim, oracle, p, op):
+    """MAX/MIN on floats depend on the operand order (NaN, signed zeros), and the order
+    of an element's tree depends on the block that owns it: a chunk pipeline would move
+    block boundaries, so a float MAX/MIN host call >= 16 MiB must stay one call."""
+    ins = oracle.random_inputs(p, (1 << 22) + 77, seed=p + 40 * op)
+    rng = np.random.default_rng(p + op)
+    for x in ins:
+        k = rng.integers(0, x.size, 1 << 16)
+        x[k[: 1 << 15]] = np.nan
+        x[k[1 << 15:]] = rng.choice(np.array([0.0, -0.0], dtype=np.float32), 1 << 15)
+    _cmp(oracle.rabenseifner, "raben", ins, op=op)
