@@ -463,6 +463,8 @@ int64_t ftar_peer_pub(ftar_comm *c, int w)
 }
 
 int ftar_is_dead(ftar_comm *c, int w) { return ftar_ctrl_is_dead(&c->job, w); }
+void ftar_enter(ftar_comm *c) { ftar_ctrl_enter(&c->job); }
+int ftar_peer_entered(ftar_comm *c, int w) { return ftar_ctrl_peer_entered(&c->job, w); }
 
 int ftar_drain(ftar_comm *c)
 {

@@ -249,6 +249,24 @@ uint64_t ftar_ctrl_agree(ftar_job *job, uint64_t members)
     }
 }
 
+void ftar_ctrl_enter(ftar_job *job)
+{
+    atomic_store_explicit(&job->shm->slot[job->rank].entered, job->seq + 1, memory_order_release);
+}
+
+int ftar_ctrl_peer_entered(ftar_job *job, int m)
+{
+    const uint64_t tok = job->seq + 1;
+    ftar_slot *s = &job->shm->slot[m];
+    for (;;) {
+        if (atomic_load_explicit(&s->entered, memory_order_acquire) >= tok) return 1;
+        /* entering happens before dying: re-read after the death test */
+        if (ftar_ctrl_is_dead(job, m)) return atomic_load_explicit(&s->entered, memory_order_acquire) >= tok;
+        if (atomic_load_explicit(&job->shm->abort_flag, memory_order_acquire)) exit_aborted(job);
+        cpu_relax();
+    }
+}
+
 void ftar_ctrl_wait_peers_arrived(ftar_job *job, uint64_t members, uint64_t seq)
 {
     double t0 = now_s();

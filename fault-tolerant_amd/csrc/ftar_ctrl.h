@@ -25,7 +25,7 @@
 #include "ftar_dev.h"
 
 #define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
-#define FTAR_SHM_VERSION 1
+#define FTAR_SHM_VERSION 2
 #define FTAR_NBUF 4       /* exported workspace buffers per rank (IN, W, T, R) */
 #define FTAR_DECISIONS 64 /* ring of agree decisions */
 
@@ -55,6 +55,10 @@ typedef struct {
     uint64_t uoff;                            /* sbuf's byte offset in the allocation */
     uint64_t useq;                            /* the call (1, 2, ...) these fields belong to */
     uint64_t ufail;                           /* call in which this rank failed to map a peer's */
+    /* exchange entry: set to seq + 1 when the rank passes an exchange step's BEFORE
+     * point (the agree sequence number is uniform at every step), so a partner decides
+     * "the exchange failed" only for a rank that died before entering it */
+    _Atomic uint64_t entered;
     char pad[64];
 } ftar_slot;
 
@@ -97,6 +101,11 @@ uint64_t ftar_ctrl_failed(ftar_job *job);
 /* Agree round over `members` (bit mask of original ranks, must contain self).
  * Returns the sealed failure snapshot (subset of members).  Never returns on abort. */
 uint64_t ftar_ctrl_agree(ftar_job *job, uint64_t members);
+/* This rank enters the exchange that precedes round seq + 1. */
+void ftar_ctrl_enter(ftar_job *job);
+/* Wait until original rank m entered the exchange this rank is in (1) or died before
+ * entering it (0).  Never returns on abort. */
+int ftar_ctrl_peer_entered(ftar_job *job, int m);
 /* Block until every member other than self arrived at round `seq` or is dead. */
 void ftar_ctrl_wait_peers_arrived(ftar_job *job, uint64_t members, uint64_t seq);
 

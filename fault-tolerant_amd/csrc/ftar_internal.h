@@ -121,6 +121,11 @@ int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, in
 int ftar_run_bg(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
 int ftar_drain_bg(ftar_comm *c);
 int ftar_is_dead(ftar_comm *c, int w);
+/* Exchange entry (see ftar_ctrl_enter): a partner's exchange failed iff it died before
+ * entering it -- what the reference's failed Sendrecv means -- independent of when the
+ * death is noticed (a rank that dies after its exchange point is still read). */
+void ftar_enter(ftar_comm *c);
+int ftar_peer_entered(ftar_comm *c, int w);
 
 /* deterministic fault injection at (phase, step, point) */
 void ftar_maybe_die(ftar_comm *c, int phase, int step, int point);

@@ -521,10 +521,11 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         memset(&xs, 0, sizeof(xs));
         rb_plan(x, step, mask, 0, &P);
         ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BEFORE);
+        ftar_enter(c);
         int skip = 0;
         if (x->vrank != -1) {
             int pw = c->order[rb_real(x, x->vrank ^ mask)];
-            if (ftar_is_dead(c, pw)) skip = x->corr = 1; /* the exchange failed (:238-241) */
+            if (!ftar_peer_entered(c, pw)) skip = x->corr = 1; /* the exchange failed (:238-241) */
             c->stats.steps++;
         }
         double lb0 = ftar_link_bytes(c);
@@ -570,9 +571,10 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         ftar_xstate xs;
         rb_plan(x, step, mask, 1, &P);
         ftar_maybe_die(c, FTAR_PH_AG, step, FTAR_PT_BEFORE);
+        ftar_enter(c);
         int skip = 0;
         if (x->vrank != -1) {
-            skip = ftar_is_dead(c, c->order[rb_real(x, x->vrank ^ mask)]);
+            skip = !ftar_peer_entered(c, c->order[rb_real(x, x->vrank ^ mask)]);
             c->stats.steps++;
         }
         /* last step: this rank's own final half W -> rbuf rides in the same launch */

@@ -250,9 +250,10 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
             P.npull[cr] = 1;
         }
         ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BEFORE);
+        ftar_enter(c);
         int skip = 0;
         if (i >= 0) {
-            skip = ftar_is_dead(c, x->active[i ^ distance]); /* corrupted (:35-49 ignore the error) */
+            skip = !ftar_peer_entered(c, x->active[i ^ distance]); /* corrupted (:35-49 ignore the error) */
             c->stats.steps++;
         }
         double lb0 = ftar_link_bytes(c);

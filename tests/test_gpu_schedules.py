@@ -75,6 +75,22 @@ def test_rd_single_kill(oracle, kill):
     _check(oracle.recursive_doubling, "rd", oracle.random_inputs(p, 65536 + 3, seed=4), [kill])
 
 
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("kill", [(0, 1, 1, 0), (3, 1, 1, 0), (4, 1, 1, 1), (2, 1, 1, 1), (0, 2, 0, 0), (4, 2, 0, 1)])
+def test_kill_operand_order_specials(oracle, algo, kill):
+    """A partner's exchange failed iff the victim died before entering it (exchange
+    entry in the control block), not whenever its death was noticed: with MAX over NaN /
+    signed zeros / infinities the replayed state's operand order shows which path ran,
+    so survivors must match the oracle bit for bit (p = 5: 4 + one idle spare)."""
+    p = 5
+    ins = H.with_specials(oracle.random_inputs(p, 65536 + 5, seed=p + 77), p + 3)
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    o = fn(ins, [kill], op=2)
+    if o.aborted or oracle.DEAD not in o.status:
+        pytest.skip("not a recovering kill point for this schedule")
+    _check(fn, algo, ins, [kill], op=2)
+
+
 def test_rd_spare_branch_p6(oracle):
     """Non power of two: an active death is repaired by waking the spare (deviation from
     the reference, which spins forever at rd/errhandler.c:100-111)."""

@@ -429,3 +429,47 @@ def test_host_pipeline_operand_order(hostsim, oracle, p, op):
         x[k[: 1 << 15]] = np.nan
         x[k[1 << 15:]] = rng.choice(np.array([0.0, -0.0], dtype=np.float32), 1 << 15)
     _cmp(oracle.rabenseifner, "raben", ins, op=op)
+
+
+SPECIAL_TRANSPORTS = {
+    "default": {},
+    "relay": RELAY_ALL,
+    "direct": {"FTAR_RELAY": "0", "FTAR_MESH": "0"},
+    "direct_serial": {"FTAR_RELAY": "0", "FTAR_MESH": "0", "FTAR_OVERLAP": "0"},
+    "copy_engine": CE,
+    "reference_shape": {"FTAR_RELAY": "0", "FTAR_MESH": "0", "FTAR_OVERLAP": "0", "FTAR_REDUNDANCY": "1"},
+}
+
+
+@pytest.mark.parametrize("transport", sorted(SPECIAL_TRANSPORTS))
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [2, 3, 5, 8, 9])
+def test_operand_order_specials(hostsim, oracle, transport, algo, p):
+    """MAX/MIN on floats with NaN and signed zeros pin the operand order of every
+    combination -- for both schedules, spare layouts (p = 3, 5, 9) and every transport,
+    not only the mesh."""
+    for op, dt in ((2, np.float32), (3, np.float64)):
+        ins = H.with_specials(oracle.random_inputs(p, 4099, seed=p * 13 + op, dtype=dt), p + 7 * op)
+        _cmp(_fn(oracle, algo), algo, ins, op=op, env=dict(SPECIAL_TRANSPORTS[transport], FTAR_RELAY_MIN="0")
+             if transport != "default" else None)
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p,op", [(5, 2), (6, 3), (9, 2)])
+def test_operand_order_specials_recovery(hostsim, oracle, algo, p, op):
+    """The recovery paths (impersonation replay, spare promotion, RD block selection)
+    keep the operand order too: every kill point the oracle recovers from, MAX/MIN with
+    NaN / signed zeros / infinities, bit-exact on every survivor."""
+    ins = H.with_specials(oracle.random_inputs(p, 1031, seed=p + 77), p + 3)
+    fn = _fn(oracle, algo)
+    n = 0
+    for v in range(p):
+        for ph in range(4):
+            for st in range(3):
+                for pt in range(3):
+                    o = fn(ins, [(v, ph, st, pt)], op=op)
+                    if o.aborted or oracle.DEAD not in o.status:
+                        continue
+                    _cmp(fn, algo, ins, [(v, ph, st, pt)], op=op)
+                    n += 1
+    assert n > 0
