@@ -190,8 +190,12 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
             memcpy(x->sindex, dsi, sizeof(dsi));
             memcpy(x->rcount, drc, sizeof(drc));
             memcpy(x->scount, dsc, sizeof(dsc));
+            /* the dead rank's whole reduce-scatter state, not only its current window: a
+             * later replay (a second failure) pulls this rank's sindex[s] windows of the
+             * steps s <= fs, which all lie in the step-0 window (the reference ships the
+             * whole buffer, :213-241) */
             void *W = c->ws[WS_W];
-            run_copy(x, at(x, W, dri[fs]), at(x, OW, dri[fs]), drc[fs], FDEV_REMOTE_X, FDEV_TAG_RECOV);
+            run_copy(x, at(x, W, dri[0]), at(x, OW, dri[0]), drc[0], FDEV_REMOTE_X, FDEV_TAG_RECOV);
             x->has_recov = 0;
         }
         ftar_drain(c);

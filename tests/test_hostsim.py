@@ -473,3 +473,28 @@ def test_operand_order_specials_recovery(hostsim, oracle, algo, p, op):
                     _cmp(fn, algo, ins, [(v, ph, st, pt)], op=op)
                     n += 1
     assert n > 0
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_raben_two_failures_random(hostsim, oracle, seed):
+    """Two failures at different steps (p = 11, three idle spares): the first recovery's
+    new entry must hold the dead rank's whole reduce-scatter state, because the second
+    recovery's replay pulls its sindex windows of earlier steps.  It held only the
+    current window and the result lost a block's contributions (SUM 40 instead of 55)."""
+    import random
+    rnd = random.Random(seed)
+    p = 11
+    pts = [(v, ph, st, pt) for v in range(p) for ph in (1, 2) for st in range(3) for pt in range(3)]
+    ins = H.with_specials(oracle.random_inputs(p, 1031, seed=p + seed), p + seed)
+    n = 0
+    for ks in [((4, 1, 1, 2), (0, 1, 2, 1)), ((8, 1, 2, 0), (10, 1, 1, 0))] + [tuple(rnd.sample(pts, 2))
+                                                                            for _ in range(60)]:
+        if ks[0][0] == ks[1][0]:
+            continue
+        for op in (0, 2):
+            o = oracle.rabenseifner(ins, list(ks), op=op)
+            if o.aborted or sum(st == oracle.DEAD for st in o.status) < 2:
+                continue
+            _cmp(oracle.rabenseifner, "raben", ins, list(ks), op=op)
+            n += 1
+    assert n > 0
