@@ -94,7 +94,7 @@ void ftar_maybe_die(ftar_comm *c, int phase, int step, int point)
         if (k->rank != c->wrank || k->phase != phase || k->step != step || k->point != point) continue;
         if (c->kill_call[i] >= 0 && c->kill_call[i] != c->ncalls - 1) continue;
         if (point == FTAR_PT_BARRIER) /* let every peer finish the step first */
-            ftar_ctrl_wait_peers_arrived(&c->job, c->members, c->job.seq + 1);
+            ftar_ctrl_wait_peers_before_dying(&c->job, c->members, c->job.seq + 1);
         if (c->verbose) fprintf(stderr, "ftar: rank %d dies at phase %d step %d point %d\n", c->wrank, phase, step, point);
         fflush(stdout);
         fflush(stderr);

@@ -267,6 +267,26 @@ int ftar_ctrl_peer_entered(ftar_job *job, int m)
     }
 }
 
+void ftar_ctrl_wait_peers_before_dying(ftar_job *job, uint64_t members, uint64_t seq)
+{
+    ftar_shm *S = job->shm;
+    atomic_store_explicit(&S->slot[job->rank].dying, seq, memory_order_release);
+    for (;;) {
+        int done = 1;
+        for (int m = 0; m < job->size && done; m++) {
+            if (m == job->rank || !(members & (1ull << m))) continue;
+            ftar_slot *s = &S->slot[m];
+            if (atomic_load_explicit(&s->arrive, memory_order_acquire) >= seq) continue;
+            if (atomic_load_explicit(&s->dying, memory_order_acquire) >= seq) continue;
+            if (ftar_ctrl_is_dead(job, m)) continue;
+            done = 0;
+        }
+        if (done) return;
+        if (atomic_load_explicit(&S->abort_flag, memory_order_acquire)) exit_aborted(job);
+        cpu_relax();
+    }
+}
+
 void ftar_ctrl_wait_peers_arrived(ftar_job *job, uint64_t members, uint64_t seq)
 {
     double t0 = now_s();

@@ -59,6 +59,8 @@ typedef struct {
      * point (the agree sequence number is uniform at every step), so a partner decides
      * "the exchange failed" only for a rank that died before entering it */
     _Atomic uint64_t entered;
+    /* BARRIER kill point (tests): reached round `dying`'s barrier and will die there */
+    _Atomic uint64_t dying;
     char pad[64];
 } ftar_slot;
 
@@ -106,6 +108,10 @@ void ftar_ctrl_enter(ftar_job *job);
 /* Wait until original rank m entered the exchange this rank is in (1) or died before
  * entering it (0).  Never returns on abort. */
 int ftar_ctrl_peer_entered(ftar_job *job, int m);
+/* BARRIER kill point: mark this rank as dying at round seq, then block until every
+ * other member arrived at round seq, is dead, or is dying at the same round (two victims
+ * of one step must not wait for each other). */
+void ftar_ctrl_wait_peers_before_dying(ftar_job *job, uint64_t members, uint64_t seq);
 /* Block until every member other than self arrived at round `seq` or is dead. */
 void ftar_ctrl_wait_peers_arrived(ftar_job *job, uint64_t members, uint64_t seq);
 

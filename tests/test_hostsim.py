@@ -498,3 +498,15 @@ def test_raben_two_failures_random(hostsim, oracle, seed):
             _cmp(oracle.rabenseifner, "raben", ins, list(ks), op=op)
             n += 1
     assert n > 0
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("ks", [((1, 1, 2, 2), (6, 1, 2, 2)), ((8, 1, 2, 2), (6, 1, 2, 2)), ((3, 1, 1, 2), (9, 1, 1, 2))])
+def test_two_barrier_victims_same_step(hostsim, oracle, algo, ks):
+    """Two ranks killed at the same step's BARRIER point: each waits for the others to
+    finish the step, but not for the other victim (they used to wait for each other
+    forever); the job then recovers or aborts like the oracle."""
+    p = 11
+    ins = H.with_specials(oracle.random_inputs(p, 1031, seed=p + 78), p + 4)
+    for op in (0, 2):
+        _cmp(_fn(oracle, algo), algo, ins, list(ks), op=op)
