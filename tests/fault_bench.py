@@ -6,7 +6,7 @@ call 0 warm-up, call 1 carries the kill (when given), call 2 runs on the survivo
 Reports per-call wall time of rank 0 for the no-fault job and the fault job, and checks
 every survivor's result against the oracle.
 
-usage: python tools/fault_bench.py [count] [victim phase step point]
+usage: python tests/fault_bench.py [count] [victim phase step point]
 FTAR_FB_RANKS=p changes the rank count (default 9).  More than 8 rank processes on the
 one GPU exceed its hardware contexts and get time-sliced (calls of 0.1-30 s); p = 5
 (4 + one idle spare) keeps the C5 structure within them.

@@ -1,0 +1,73 @@
+"""Random multi-failure sweep on the host-sim: the product vs the oracle, bit for bit.
+
+Draws sets of kill points ((rank, phase, step, point), distinct ranks) at random, keeps
+those the oracle recovers from with the requested number of deaths, and runs each through
+the host-sim build of the library (real processes, the product's host C).  MAX/MIN over
+NaN / signed zeros / infinities pin the operand order of every combination, so a
+recovery that takes a different path than the oracle shows up even when the values agree.
+This sweep found the new-entry state hand-off and the BARRIER co-victim wait (DESIGN.md
+§3, "Second failure after a promotion").
+
+usage: python tests/fault_sweep.py [--p 11] [--kills 2] [--draws 400] [--seed 3] [--jobs 6]
+"""
+import argparse
+import os
+import random
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import harness as H  # noqa: E402
+import oracle as O  # noqa: E402
+
+
+def run_one(algo, p, op, kills, count):
+    ins = H.with_specials(O.random_inputs(p, count, seed=p + 78), p + 4)
+    fn = O.rabenseifner if algo == "raben" else O.recursive_doubling
+    o = fn(ins, list(kills), op=op)
+    if o.aborted or sum(s == O.DEAD for s in o.status) < len(kills):
+        return None
+    try:
+        r = H.run_probe(algo, ins, list(kills), op=op, backend="hostsim", timeout=30)
+    except Exception:
+        return "hang"
+    if r.aborted:
+        return "aborted"
+    bad = [w for w in range(p) if o.status[w] == 0 and
+           (w not in r.outputs or not np.array_equal(r.outputs[w][0].view(np.uint32), o.outputs[w].view(np.uint32)))]
+    return bad or "ok"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--p", type=int, default=11)
+    ap.add_argument("--kills", type=int, default=2)
+    ap.add_argument("--draws", type=int, default=400)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--count", type=int, default=1031)
+    ap.add_argument("--jobs", type=int, default=6)
+    a = ap.parse_args()
+    rnd = random.Random(a.seed)
+    pts = [(v, ph, st, pt) for v in range(a.p) for ph in (1, 2) for st in range(3) for pt in range(3)]
+    cases = []
+    for algo in ("raben", "rd"):
+        for _ in range(a.draws):
+            ks = tuple(rnd.sample(pts, a.kills))
+            if len({k[0] for k in ks}) == a.kills:
+                cases.append((algo, a.p, rnd.choice([0, 2, 3]), ks, a.count))
+    with ThreadPoolExecutor(a.jobs) as ex:
+        res = list(ex.map(lambda c: run_one(*c), cases))
+    ran = [(c, r) for c, r in zip(cases, res) if r is not None]
+    bad = [(c, r) for c, r in ran if r != "ok"]
+    print(f"{len(cases)} drawn, {len(ran)} recovering with {a.kills} deaths, {len(bad)} differ from the oracle")
+    for c, r in bad[:20]:
+        print("  ", c[0], "op", c[2], "kills", c[3], "->", r)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
