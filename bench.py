@@ -7,11 +7,17 @@ fault-tolerant Allreduce.
 
 N = 1: the single-GPU workload of BASELINE.json configs[1] -- the local-reduce HIP
        kernel (MPI_Reduce_local, the per-step bucket reduction) on two 256 MiB float32
-       vectors.  One step = one kernel launch.  HBM-bound.
+       vectors.  One step = one kernel launch.  HBM-bound.  The timed launches rotate
+       over --pairs vector pairs (default 4 = 2 GiB) so no launch finds its operands in
+       the 256 MiB Infinity Cache the previous launches filled: an HBM number.
 N > 1: configs[3] -- fault-tolerant Rabenseifner Allreduce of a 256 MiB float32 vector
        per rank, one rank per GPU, exchanges pulled over xGMI (weak scaling: every rank
-       contributes one 256 MiB vector).  One step = one Allreduce.  Recursive doubling
-       (configs[2]) and RCCL's all_reduce on the same buffers are reported beside it.
+       contributes one 256 MiB vector).  One step = one Allreduce.  The schedule and
+       transport that ran are named in `config`; the reference's own data movement
+       (pairwise, step by step, step-0 full exchange) is timed as `reference_shape`.
+       Recursive doubling (configs[2]), RCCL's all_reduce, a size sweep 4 B - 256 MiB
+       (FT vs RCCL), the host-C CPU port of the schedule, and configs[4] (9 ranks = N
+       GPUs + one idle spare, a kill mid-exchange, recovery) are reported beside it.
 
 value = (input vectors summed x bytes per vector) / time per step, whole job:
         N=1: 2 x 256 MiB per launch; N>1: N x 256 MiB per Allreduce.
@@ -21,6 +27,7 @@ import argparse
 import importlib.util
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -29,6 +36,8 @@ COUNT = 1 << 26              # 256 MiB of float32 per vector
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 76.8         # one xGMI link, one direction (153.6 GB/s bidirectional spec)
 METRIC = "Allreduce GB/s (device-resident, float32 SUM) at 1/2/4/8 MI355X"
+# data/data_fault/log_single_Raben.csv, N = 9, OK runs: median clock() seconds
+REF_C5_S = {"kill": 1.334, "no_kill": 1.329, "count": 120732254}
 
 
 def load_package():
@@ -36,6 +45,13 @@ def load_package():
     spec = importlib.util.spec_from_file_location("ftar_amd", path)
     mod = importlib.util.module_from_spec(spec)
     sys.modules["ftar_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_tool(name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "tools", name + ".py"))
+    mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
 
@@ -73,44 +89,74 @@ def cpu_baseline_local_reduce(min_seconds=10.0, max_passes=2000):
                       f"({dt:.1f} s), 1 host thread"}
 
 
+def cpu_schedule(algo, p, count, reps):
+    """The schedule on the host cores: the product's host C (control plane, agree rounds,
+    the FT schedule) as p processes pinned one per core, POSIX shared memory as the
+    transport, C loops as the reduce (tools/cpu_schedule_bench.py), float32."""
+    cs = load_tool("cpu_schedule_bench")
+    cs.build()
+    r = cs.run(algo, p, count, "float32", reps)
+    return r, cs.cpu_model()
+
+
+def c1_baseline():
+    """BASELINE configs[0]: src/rd/main recursive doubling, float32 SUM, 64 KiB, 4 ranks."""
+    r, model = cpu_schedule("rd", 4, 16384, 20)
+    return {"value": round(4 * 16384 * 4 / r["time_s"] / 1e9, 4), "unit": "GB/s", "ms_per_call": round(r["time_s"] * 1e3, 4),
+            "algbw_GBps": r["algbw_GBps"], "cores": 4, "kind": "port", "cpu_model": model,
+            "sample": "configs[0]: recursive doubling, 64 KiB float32 SUM per rank, 4 rank processes pinned one "
+                      "per core, pairwise step-by-step exchanges through shared memory, median of 20 runs "
+                      "(value = 4 x 64 KiB / call time, as the GPU lines)",
+            "reference_leonardo_ms": 0.976}
+
+
 def single(args):
     import torch
     ftar = load_package()
     ftar.lib()
     torch.cuda.set_device(0)
     g = torch.Generator(device="cuda").manual_seed(42)
-    x = torch.rand(args.count, device="cuda", generator=g) * 2 - 1
-    y = torch.rand(args.count, device="cuda", generator=g) * 2 - 1
+    pairs = [(torch.rand(args.count, device="cuda", generator=g) * 2 - 1,
+              torch.rand(args.count, device="cuda", generator=g) * 2 - 1) for _ in range(args.pairs)]
     ftar.set_reduce_variant(args.variant)
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
+        x, y = pairs[k % args.pairs]
         ftar.reduce_local(x, y)
     torch.cuda.synchronize()
-    if args.timing == "launch":
-        # an event pair around every launch: per-launch kernel time, at the cost of two
-        # timestamp markers between consecutive kernels in the timed region
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
-        t0 = time.perf_counter()
-        for e0, e1 in evs:
-            e0.record()
-            ftar.reduce_local(x, y)  # launched on torch's current stream, the one the events see
-            e1.record()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        k_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
-    else:
-        # one event pair around the whole timed region: the average launch duration
-        # includes the kernel-to-kernel boundaries, nothing is inserted between launches
+
+    def region(steps, npairs):
+        # one event pair around the whole timed region, on the stream the kernels run on
+        # (torch's current stream, which reduce_local launches on): the average launch
+        # duration includes the kernel-to-kernel boundaries, nothing runs in between
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         e0.record()
-        for _ in range(args.steps):
+        for k in range(steps):
+            x, y = pairs[k % npairs]
             ftar.reduce_local(x, y)
         e1.record()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        k_ms = e0.elapsed_time(e1) / args.steps
-    ms_step = (t1 - t0) * 1e3 / args.steps
+        return (t1 - t0) * 1e3 / steps, e0.elapsed_time(e1) / steps
+
+    if args.timing == "launch":
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for k, (e0, e1) in enumerate(evs):
+            x, y = pairs[k % args.pairs]
+            e0.record()
+            ftar.reduce_local(x, y)
+            e1.record()
+        torch.cuda.synchronize()
+        ms_step = (time.perf_counter() - t0) * 1e3 / args.steps
+        k_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / args.steps
+    else:
+        ms_step, k_ms = region(args.steps, args.pairs)
+    # the same launches on ONE pair (operands partly left in the Infinity Cache by the
+    # previous launch): what round 1 timed; reported, not the headline
+    _, k_same = region(min(args.steps, 100), 1)
     S = args.count * 4
     achieved = 3 * S / (k_ms * 1e-3) / 1e9
     out = {
@@ -119,16 +165,27 @@ def single(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic uniform[-1,1), HBM-resident",
         "config": {"workload": "configs[1]: local-reduce HIP kernel (MPI_Reduce_local), 2 x 256 MiB float32 SUM, "
                                "1 MI355X", "count": args.count, "kernel_variant": args.variant,
-                   "timing": args.timing},
+                   "timing": args.timing,
+                   "buffers": f"{args.pairs} rotating pairs ({args.pairs * 2 * S >> 20} MiB working set, "
+                              f"beyond the 256 MiB Infinity Cache)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic("reduce_local_c2_lds" if args.variant == 1 else "reduce_local_c2"),
+                     "traffic": pmc_traffic("reduce_local_c2_lds_rot" if args.variant == 1 else "reduce_local_c2_rot"),
                      "kernel": "reduce_lds_kernel<float,SUM>" if args.variant == 1 else "segment_kernel<float,SUM>",
                      "algorithmic_bytes_per_launch": 3 * S,
-                     "kernel_ms": round(k_ms, 4)},
+                     "kernel_ms": round(k_ms, 4),
+                     "same_pair_kernel_ms": round(k_same, 4),
+                     "same_pair_GBps": round(3 * S / (k_same * 1e-3) / 1e9, 1)},
     }
     out["e2e"] = e2e_local(ftar, args.count)
-    out["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_local_reduce()
+    if args.no_cpu_baseline:
+        out["cpu_baseline"] = None
+    else:
+        out["cpu_baseline"] = cpu_baseline_local_reduce()
+        try:
+            out["cpu_baseline"]["c1"] = c1_baseline()
+        except Exception as e:  # reported, never fatal: the GPU line stands on its own
+            out["cpu_baseline"]["c1"] = {"error": str(e)[-300:]}
     print(json.dumps(out), flush=True)
 
 
@@ -163,6 +220,60 @@ def e2e_local(ftar, count, iters=5):
             "GBps": round(2 * S * iters / ts["total"] / 1e9, 2)}
 
 
+def c5_leg(world, devices, count, ranks):
+    """configs[4] on this node: `ranks` = world GPUs' worth of ranks + one idle spare (rank
+    1 shares rank 0's GPU), Rabenseifner 256 MiB float32 SUM, three calls per job; the
+    fault job kills vrank 5 (original rank 6) in reduce-scatter step 1 of call 1, mid-
+    exchange (its own pull kernel in flight, its partner's pull reading its HBM).  The
+    recovery shrinks the comm; call 2 runs on the survivors.  Run by rank 0 as a separate
+    ftrun job of bin/ftbench: torchrun's agent would tear the job down on a SIGKILL."""
+    exe = os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftbench")
+    ftrun = os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftrun")
+    devmap = [devices[0], devices[0]] + [devices[(r - 1) % len(devices)] for r in range(2, ranks)]
+    victim = 6 if ranks > 6 else ranks - 1
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith(("FTAR_", "RANK", "LOCAL_", "WORLD_", "GROUP_", "ROLE_", "TORCHELASTIC"))}
+    res = {"ranks": ranks, "devmap": devmap, "count": count, "calls": 3,
+           "kill": f"{victim}:1:1:3 in call 1 (original rank {victim} = vrank {victim - 1}, reduce-scatter step 1, "
+                   "mid-exchange)"}
+    want_all = float(sum(range(ranks)))
+    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:1")):
+        e = dict(env)
+        if kill:
+            e["FTAR_KILL"] = kill
+        t0 = time.time()
+        cp = subprocess.run([ftrun, "-np", str(ranks), "--devmap", ",".join(map(str, devmap)), exe, "raben",
+                             str(count), "3"], env=e, capture_output=True, text=True, timeout=600)
+        lines = [json.loads(l) for l in cp.stdout.splitlines() if l.startswith("{")]
+        calls = []
+        for c in range(3):
+            per = [ln["calls"][c] for ln in lines]
+            want = want_all - (victim if (kill and c == 2) else 0)
+            calls.append({"ms_max_over_ranks": round(max(p["ms"] for p in per), 3) if per else None,
+                          "recoveries": max((p["recoveries"] for p in per), default=None),
+                          "comm_size_after": min((p["comm_size"] for p in per), default=None),
+                          "result_ok": bool(per) and all(p["rc"] == 0 and p["uniform"] and p["value"] == want
+                                                         for p in per)})
+        res[name] = {"rc": cp.returncode, "survivors": len(lines), "job_wall_s": round(time.time() - t0, 2),
+                     "calls": calls}
+        if cp.returncode != 0 or not lines:
+            res[name]["stderr_tail"] = cp.stderr[-600:]
+        mid = [l for l in cp.stderr.splitlines() if "dies mid-exchange" in l]
+        if mid:
+            res[name]["victim"] = mid[0].split("ftar: ")[-1]
+    f, n = res.get("fault", {}), res.get("no_fault", {})
+    try:
+        res["recovered"] = f["survivors"] == ranks - 1 and f["calls"][1]["recoveries"] == 1 and \
+            all(c["result_ok"] for c in f["calls"])
+        res["recovered_call_ms"] = f["calls"][1]["ms_max_over_ranks"]
+        res["no_fault_call_ms"] = n["calls"][1]["ms_max_over_ranks"]
+        res["recovery_overhead_ms"] = round(res["recovered_call_ms"] - res["no_fault_call_ms"], 3)
+    except (KeyError, IndexError, TypeError):
+        res["recovered"] = False
+    res["reference_leonardo_s"] = dict(REF_C5_S, note="clock() s per run incl. the whole MPI job, 460.6 MiB int32")
+    return res
+
+
 def multi(args):
     import torch
     import torch.distributed as dist
@@ -172,6 +283,7 @@ def multi(args):
     local = int(os.environ.get("LOCAL_RANK", rank))
     # FTAR_DEVICE pins every rank to one GPU (single-GPU rehearsal of the multi-rank path;
     # RCCL refuses two ranks on one device, so such runs use --dist-backend gloo)
+    rehearsal = "FTAR_DEVICE" in os.environ  # every rank on one GPU
     dev = int(os.environ.get("FTAR_DEVICE", local)) % max(1, torch.cuda.device_count())
     os.environ.setdefault("FTAR_DEVICE", str(dev))  # the library opens the same device
     torch.cuda.set_device(dev)
@@ -182,27 +294,34 @@ def multi(args):
     x = torch.rand(args.count, device="cuda", generator=g) * 2 - 1
     y = torch.empty_like(x)
     S = args.count * 4
+    nccl = args.dist_backend == "nccl"
 
-    def timed(fn):
-        for _ in range(args.warmup):
+    def max_over_ranks(vals):
+        t = torch.tensor(vals, dtype=torch.float64)
+        if nccl:
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [v.item() for v in t.cpu()]
+
+    def timed(fn, steps=None, warmup=None):
+        steps = args.steps if steps is None else steps
+        warmup = args.warmup if warmup is None else warmup
+        for _ in range(warmup):
             fn()
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         step0 = 0.0
-        for _ in range(args.steps):
+        for _ in range(steps):
             fn()
             step0 += comm.last_stats().step0_kernel_ms
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         dist.barrier()
-        t = torch.tensor([t1 - t0, step0], dtype=torch.float64)
-        if args.dist_backend == "nccl":
-            t = t.cuda()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t, k = max_over_ranks([t1 - t0, step0])
         timed.link_bytes = comm.last_stats().step0_link_bytes
-        return t[0].item() / args.steps, t[1].item() / args.steps
+        return t / steps, k / steps
 
     def raben():
         rc = comm.allreduce_rabenseifner(x, y)
@@ -213,12 +332,14 @@ def multi(args):
         assert rc == 0, rc
 
     def quick(fn, steps=3, warmup=1):
-        saved = (args.steps, args.warmup)
-        args.steps, args.warmup = steps, warmup
-        try:
-            return timed(fn)[0]
-        finally:
-            args.steps, args.warmup = saved
+        return timed(fn, steps, warmup)[0]
+
+    opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY, ftar.OPT_MESH)
+    defaults = {o: comm.get_option(o) for o in opts}
+
+    def set_opts(vals):
+        for o, v in zip(opts, vals):
+            comm.set_option(o, v)
 
     # Transport selection before the timed run: how the node's xGMI links behave under
     # concurrent peer reads decides between the one-hop mesh (power-of-two p without a
@@ -250,9 +371,11 @@ def multi(args):
     relayed = comm.last_stats().relayed_steps > 0
     meshed = comm.last_stats().mesh_steps > 0
     oneshot = comm.last_stats().mesh_steps == 1  # the mesh's one-launch form (p = 2, small vectors)
+    transport = "mesh-oneshot" if oneshot else "mesh" if meshed else "relay2hop" if relayed else "direct"
+    chosen_opts = {o: comm.get_option(o) for o in opts}
     # correctness spot check against torch.distributed's all_reduce on the same inputs
     # (fp32, different reduction order: |err| <= log2(p) * 2^-24 * sum|x_i|)
-    ref = x.clone() if args.dist_backend == "nccl" else x.cpu()
+    ref = x.clone() if nccl else x.cpu()
     dist.all_reduce(ref)
     raben()
     err = (y.cpu() - ref.cpu()).abs().max().item()
@@ -266,6 +389,12 @@ def multi(args):
     cks_rd = int((yi.to(torch.int64) % 17).sum().item())
     cks_want = ((world * (world - 1) // 2) % 17) * args.count
     del xi, yi
+    # The reference's own data movement, first class: pairwise pulls, step by step, one
+    # link per step, with the step-0 full-vector exchange kept (its tmp redundancy,
+    # raben/rabenseifner.c:206-211) even where no handler can use it.
+    set_opts((0, 0, 0, 1, 0))
+    t_ref, k_ref = timed(raben)
+    set_opts([chosen_opts[o] for o in opts])
     # recursive doubling has no mesh form (it can recover at any p): relay or direct
     rd_selection = None
     relay_for_raben = comm.get_option(ftar.OPT_RELAY)
@@ -279,41 +408,39 @@ def multi(args):
                         "chosen": "relay2hop" if t_r <= t_d else "direct"}
     t_rd, k_rd = timed(rd)
     comm.set_option(ftar.OPT_RELAY, relay_for_raben)
-    # the same schedules over plain pairwise exchanges (one link per step), with and
-    # without the background-stream redundancy copy -- the reference's transport shape
+    # the same schedules over the other transports
     transports = {}
     if not args.no_variants:
-        opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY, ftar.OPT_MESH)
-        defaults = {o: comm.get_option(o) for o in opts}
         # mesh: one-hop reduce-scatter + allgather (power-of-two p, no spare); relay2hop:
         # the step-by-step schedule striped over 2-hop paths; direct: one pull kernel per
         # step; direct_serial: plus the step-0 copy inline; copy_engine: hipMemcpyAsync of
-        # the partner's window + a local reduce kernel; reference_shape: pairwise, inline,
-        # with the step-0 full exchange even where no handler can use it (the reference's
-        # data movement); relay_full_exchange: the relay with that full exchange
+        # the partner's window + a local reduce kernel; relay_full_exchange: the relay with
+        # the reference's step-0 full exchange
         variants = (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
                     ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
-                    ("reference_shape", (0, 0, 0, 1, 0)), ("relay_full_exchange", (1, 1, 0, 1, 0)))
+                    ("relay_full_exchange", (1, 1, 0, 1, 0)))
         for name, vals in variants:
-            for o, v in zip(opts, vals):
-                comm.set_option(o, v)
+            if name == "mesh" and not pow2:
+                continue
+            set_opts(vals)
             tv, _ = timed(raben)
             tv_rd, _ = timed(rd) if name in ("relay2hop", "direct", "copy_engine") else (None, None)
             transports[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2)}
             if tv_rd:
                 transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
-        for o, v in defaults.items():
-            comm.set_option(o, v)
-    # per-call time over message sizes on the node (max over ranks), with the chosen
-    # transport: the fixed cost per call and the one-shot threshold (FTAR_ONESHOT_MAX)
-    # measured one rank per GPU instead of estimated from the one-GPU rehearsals
+        set_opts([chosen_opts[o] for o in opts])
+    # Per-call time over message sizes (max over ranks), 4 B .. 256 MiB, with the chosen
+    # transport, next to RCCL's all_reduce on the same sizes: the FT/vendor curve of the
+    # reference's compare campaign (slurm/test_compare.slurm:27-50, check_compare.py),
+    # plus the fixed cost per call and the one-shot threshold (FTAR_ONESHOT_MAX)
     sizes = {}
     if not args.no_variants:
         comm.set_profiling(False)  # no kernel events: the plain per-call cost
         oneshot_max = comm.get_option(ftar.OPT_ONESHOT_MAX)
-        for n in (1 << 8, 1 << 14, 1 << 18, 1 << 20, 1 << 22):
-            if n > args.count:
-                continue
+        z = x.clone() if nccl else None
+        n = 1
+        while n <= args.count:
+            steps, warm = (20, 3) if n <= (1 << 22) else (5, 2)
             row = {"bytes": 4 * n}
             for name, fn, extra in (("raben", comm.allreduce_rabenseifner, None),
                                     ("raben_no_oneshot", comm.allreduce_rabenseifner, 0),
@@ -328,9 +455,14 @@ def multi(args):
                     rc = fn(x, y, count=n)
                     assert rc == 0, rc
 
-                row[name + "_us"] = round(quick(call, steps=20, warmup=3) * 1e6, 2)
+                row[name + "_us"] = round(quick(call, steps=steps, warmup=warm) * 1e6, 2)
                 comm.set_option(ftar.OPT_ONESHOT_MAX, oneshot_max)
+            if z is not None:
+                zn = z[:n]
+                row["rccl_us"] = round(quick(lambda: dist.all_reduce(zn), steps=steps, warmup=warm) * 1e6, 2)
+                row["raben_over_rccl"] = round(row["raben_us"] / row["rccl_us"], 3)
             sizes[str(4 * n)] = row
+            n *= 2
         comm.set_profiling(True)
     # end-to-end with host buffers: pinned H2D + device Allreduce + D2H (never the value)
     xh = x.cpu().pin_memory()
@@ -340,18 +472,35 @@ def multi(args):
         rc = comm.allreduce_rabenseifner_host(xh, yh)
         assert rc == 0, rc
 
-    saved = (args.steps, args.warmup)
-    args.steps, args.warmup = 3, 1
-    t_e2e, _ = timed(raben_host)
-    args.steps, args.warmup = saved
+    t_e2e, _ = timed(raben_host, 3, 1)
     t_nc = None
-    if args.dist_backend == "nccl":
-        z = x.clone()
-
-        def rccl():
-            dist.all_reduce(z)
-
-        t_nc, _ = timed(rccl)
+    if nccl:
+        zz = x.clone()
+        t_nc, _ = timed(lambda: dist.all_reduce(zz))
+    # The CPU baseline: the same schedule on this node's host cores, in this job, rank 0
+    # only (the others wait at the barrier), float32, the same 256 MiB per rank.
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        try:
+            r, model = cpu_schedule("raben", world, args.count, 3)
+            cpu = {"value": round(world * S / r["time_s"] / 1e9, 4), "unit": "GB/s", "cores": world, "kind": "port",
+                   "cpu_model": model, "ms_per_call": round(r["time_s"] * 1e3, 2), "algbw_GBps": r["algbw_GBps"],
+                   "sample": f"Rabenseifner (FT, the reference's step-by-step pairwise shape), {world} rank processes "
+                             f"pinned one per core, 256 MiB float32 per rank through shared memory, median of 3 "
+                             f"calls (driver Time: lines, max over ranks); value = {world} x 256 MiB / call time"}
+        except Exception as e:
+            cpu = {"value": None, "unit": "GB/s", "cores": world, "kind": "port", "sample": f"failed: {str(e)[-300:]}"}
+    dist.barrier()
+    # configs[4]: the single-kill leg, its own ftrun job (rank 0), after everything else
+    c5 = None
+    if rank == 0 and not args.no_c5:
+        # this job's GPUs (LOCAL_RANK = GPU on one node), or the one GPU of a rehearsal
+        devices = [dev] if rehearsal else list(range(world))
+        try:
+            c5 = c5_leg(world, devices, args.count, int(os.environ.get("FTAR_C5_RANKS", "9")))
+        except Exception as e:
+            c5 = {"error": str(e)[-500:]}
+    dist.barrier()
     L = world.bit_length() - 1
     r = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
     # Link bytes per rank per direction.  The reference's FT Raben moves
@@ -380,25 +529,45 @@ def multi(args):
     links = (world - 1) if meshed else (r - 1) if relayed else 1
     peak = links * XGMI_LINK_GBS
     achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernels' pulled bytes
+    schedule = {
+        "mesh-oneshot": "Rabenseifner, one-shot mesh: every block in its owner's reduction tree in one launch "
+                        "(power-of-two p, no spare)",
+        "mesh": "Rabenseifner, one-hop mesh: reduce-scatter as one tree kernel over p-1 peer pulls, allgather as "
+                "one multi-source pull (power-of-two p, no spare; same reduction tree as recursive halving)",
+        "relay2hop": "Rabenseifner, step by step (recursive halving + doubling), each exchange striped over 2-hop "
+                     "relays",
+        "direct": "Rabenseifner, step by step (recursive halving + doubling), one pairwise pull per step",
+    }[transport]
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(world * S / t_rb / 1e9, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_rb * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic uniform[-1,1), HBM-resident",
-            "config": {"workload": "configs[3]: fault-tolerant Rabenseifner Allreduce, 256 MiB float32 SUM per "
-                                   "rank, one rank per MI355X, pull exchanges over xGMI",
+            "config": {"workload": f"configs[3]: fault-tolerant Rabenseifner Allreduce, 256 MiB float32 SUM per "
+                                   f"rank, one rank per MI355X -- {schedule}",
+                       "schedule": schedule, "transport": transport,
+                       "step0_redundancy": "full exchange (reference)" if keep else
+                       "elided (no idle rank: every handler aborts, raben/errhandler.c:207-211)",
                        "count": args.count, "parallelism": f"{world} ranks"},
             "algbw_GBps": round(S / t_rb / 1e9, 2),
-            "transport": "mesh-oneshot" if oneshot else "mesh" if meshed else "relay2hop" if relayed else "direct",
+            "transport": transport,
+            "reference_shape": {
+                "schedule": "Rabenseifner step by step, pairwise pulls (one xGMI link per step), step-0 full-vector "
+                            "exchange kept (raben/rabenseifner.c:206-211)",
+                "value": round(world * S / t_ref / 1e9, 2), "ms_per_step": round(t_ref * 1e3, 4),
+                "algbw_GBps": round(S / t_ref / 1e9, 2), "step0_kernel_ms": round(k_ref, 4),
+                "survey_ft_roofline_ms": round(t_survey * 1e3, 3),
+                "frac_of_survey_roofline": round(t_survey / t_ref, 4)},
             "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "link_GBps": XGMI_LINK_GBS,
                                        "links_per_step": links, "t_roof_ms": round(t_roof * 1e3, 3),
-                                       "frac": round(t_roof / t_rb, 4),
-                                       "survey_ft_roofline_ms": round(t_survey * 1e3, 3),
-                                       "frac_of_survey_roofline": round(t_survey / t_rb, 4)},
+                                       "frac": round(t_roof / t_rb, 4)},
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
                          "peak": peak, "unit": "GB/s",
-                         "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
+                         "frac": round(achieved / peak, 4) if achieved else None,
+                         "traffic": None,
+                         "traffic_note": "PMC counters of a peer-reading kernel are per device; not collected on "
+                                         "the 8-GPU node (profiles/ has the one-GPU rehearsal's)",
                          "kernel": ("Raben one-shot mesh: tree_batch_kernel, every block in its owner's tree"
                                     if oneshot
                                     else "Raben mesh reduce-scatter: tree_kernel over p-1 one-hop pulls" if meshed
@@ -407,15 +576,17 @@ def multi(args):
                          "algorithmic_bytes_per_launch": step0_bytes, "kernel_ms": round(k_rb, 4)},
             "e2e_host_buffers": {"ms_per_step": round(t_e2e * 1e3, 3), "algbw_GBps": round(S / t_e2e / 1e9, 2)},
             "rd": {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
+                   "value": round(world * S / t_rd / 1e9, 2),
                    "step0_kernel_ms": round(k_rd, 4), "transport_selection": rd_selection},
-            "rccl_allreduce": ({"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2)}
-                               if t_nc else None),
+            "rccl_allreduce": ({"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2),
+                                "value": round(world * S / t_nc / 1e9, 2)} if t_nc else None),
             "transport_selection": selection,
             "transports": transports,
             "size_sweep_us": sizes,
             "max_abs_err_vs_rccl": err,
             "int32_rank_checksum_ok": {"raben": cks_raben == cks_want, "rd": cks_rd == cks_want},
-            "cpu_baseline": None,
+            "c5_single_kill": c5,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     comm.finalize()
@@ -428,11 +599,13 @@ def main():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--count", type=int, default=COUNT)
+    ap.add_argument("--pairs", type=int, default=4, help="N=1: rotating vector pairs (4 x 2 x 256 MiB = 2 GiB)")
     ap.add_argument("--variant", type=int, default=1, help="local-reduce kernel: 0 register, 1 LDS-DMA (default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="N>1: skip the configs[4] single-kill leg")
     ap.add_argument("--timing", choices=["region", "launch"], default="region",
                     help="N=1 kernel time: events around the timed region, or around every launch")
-    ap.add_argument("--no-variants", action="store_true", help="N>1: skip the direct-transport comparison")
+    ap.add_argument("--no-variants", action="store_true", help="N>1: skip the transport comparison and size sweep")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for barrier/timing")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))

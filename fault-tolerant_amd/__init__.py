@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libftar.so")
 INT32, FLOAT32, INT64, FLOAT64 = 0, 1, 2, 3
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
 PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
-PT_BEFORE, PT_AFTER, PT_BARRIER = 0, 1, 2
+PT_BEFORE, PT_AFTER, PT_BARRIER, PT_DURING = 0, 1, 2, 3
 OPT_OVERLAP, OPT_RELAY, OPT_RELAY_MIN, OPT_LOOP_SECONDS, OPT_COPY_ENGINE, OPT_REDUNDANCY, OPT_MESH = 0, 1, 2, 3, 4, 5, 6
 OPT_ONESHOT_MAX = 7
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75

@@ -95,6 +95,15 @@ void ftar_maybe_die(ftar_comm *c, int phase, int step, int point)
         if (c->kill_call[i] >= 0 && c->kill_call[i] != c->ncalls - 1) continue;
         if (point == FTAR_PT_BARRIER) /* let every peer finish the step first */
             ftar_ctrl_wait_peers_before_dying(&c->job, c->members, c->job.seq + 1);
+        if (point == FTAR_PT_DURING) {
+            /* mid-exchange: this rank's own pulls are queued, and once every peer has
+             * launched its pulls of the step the partners' kernels read our HBM while
+             * this process (and its queues) is torn down */
+            int peers = ftar_ctrl_wait_peers_launched(&c->job, c->members);
+            int busy = fdev_busy(c->dev);
+            fprintf(stderr, "ftar: rank %d dies mid-exchange (phase %d step %d): own kernel %s, %d peers launched\n",
+                    c->wrank, phase, step, busy ? "in flight" : "complete", peers);
+        }
         if (c->verbose) fprintf(stderr, "ftar: rank %d dies at phase %d step %d point %d\n", c->wrank, phase, step, point);
         fflush(stdout);
         fflush(stderr);
@@ -465,6 +474,15 @@ int64_t ftar_peer_pub(ftar_comm *c, int w)
 int ftar_is_dead(ftar_comm *c, int w) { return ftar_ctrl_is_dead(&c->job, w); }
 void ftar_enter(ftar_comm *c) { ftar_ctrl_enter(&c->job); }
 int ftar_peer_entered(ftar_comm *c, int w) { return ftar_ctrl_peer_entered(&c->job, w); }
+int ftar_peer_done(ftar_comm *c, int w) { return ftar_ctrl_peer_done(&c->job, w); }
+
+void ftar_launched(ftar_comm *c, int phase, int step)
+{
+    ftar_ctrl_launched(&c->job);
+    ftar_maybe_die(c, phase, step, FTAR_PT_DURING);
+}
+
+void ftar_exchange_done(ftar_comm *c) { ftar_ctrl_done(&c->job); }
 
 int ftar_drain(ftar_comm *c)
 {
@@ -592,16 +610,43 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
     return FTAR_SUCCESS;
 }
 
+/* Pinned staging of the _host entry points, grown on demand.  Every rank of the comm
+ * calls this at the start of the same collective, so a rank that cannot allocate ends the
+ * job (MPI_Abort) instead of returning alone while its peers wait in the collective's
+ * first barrier. */
+int ftar_ensure_staging(ftar_comm *c, size_t bytes)
+{
+    if (bytes == 0 || (bytes <= c->hbytes && c->hsend && c->hrecv)) return FTAR_SUCCESS;
+    fdev_free(c->dev, c->hsend);
+    fdev_free(c->dev, c->hrecv);
+    c->hsend = c->hrecv = NULL;
+    c->hbytes = 0;
+    if (fdev_alloc_plain(c->dev, bytes, &c->hsend) || fdev_alloc_plain(c->dev, bytes, &c->hrecv)) {
+        fprintf(stderr, "ftar: rank %d: staging allocation of %zu B failed: %s\n", c->wrank, bytes,
+                fdev_last_error());
+        fdev_free(c->dev, c->hsend);
+        c->hsend = NULL;
+        ftar_ctrl_abort(&c->job, FTAR_ERR_NOMEM);
+    }
+    c->hbytes = bytes;
+    return FTAR_SUCCESS;
+}
+
 /* ---- statistics ----------------------------------------------------------- */
 
 static double g_t0;
 
+/* One user call = one stats record and one call index (FTAR_KILL ':call'), also when the
+ * host pipeline runs it as several chunk Allreduces (c->chunk_cont set for chunks 2..n):
+ * their counters accumulate into the record the first chunk opened. */
 void ftar_stats_begin(ftar_comm *c)
 {
-    c->ncalls++;
-    memset(&c->stats, 0, sizeof(c->stats));
+    if (!c->chunk_cont) {
+        c->ncalls++;
+        memset(&c->stats, 0, sizeof(c->stats));
+        g_t0 = now_s();
+    }
     fdev_counters_reset(c->dev);
-    g_t0 = now_s();
 }
 
 void ftar_stats_end(ftar_comm *c)
@@ -609,12 +654,12 @@ void ftar_stats_end(ftar_comm *c)
     fdev_counters k;
     fdev_counters_get(c->dev, &k);
     c->stats.wall_s = now_s() - g_t0;
-    c->stats.kernel_ms = k.ms[0] + k.ms[1] + k.ms[2] + k.ms[3] + k.ms[4];
-    c->stats.bg_kernel_ms = k.ms[FDEV_TAG_BG];
-    c->stats.step0_kernel_ms = k.ms[FDEV_TAG_STEP0];
-    c->stats.link_bytes = k.link_bytes;
-    c->stats.hbm_bytes = k.hbm_bytes;
-    c->stats.kernels = k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3] + k.launches[4];
+    c->stats.kernel_ms += k.ms[0] + k.ms[1] + k.ms[2] + k.ms[3] + k.ms[4];
+    c->stats.bg_kernel_ms += k.ms[FDEV_TAG_BG];
+    c->stats.step0_kernel_ms += k.ms[FDEV_TAG_STEP0];
+    c->stats.link_bytes += k.link_bytes;
+    c->stats.hbm_bytes += k.hbm_bytes;
+    c->stats.kernels += k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3] + k.launches[4];
     c->stats.comm_size_after = c->size;
     ftar_inputs_done(c);
 }

@@ -18,6 +18,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <signal.h>
+#include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -200,6 +201,18 @@ static void exit_aborted(ftar_job *job)
     _exit(code ? code : 1);
 }
 
+/* A member that called ftar_finalize never arrives again: waiting for it is a protocol
+ * error (ranks ran different sequences of collectives), not a failure to recover from. */
+static void check_finalized(ftar_job *job, int m, _Atomic uint64_t *field, uint64_t seq)
+{
+    if (atomic_load_explicit(&job->shm->slot[m].state, memory_order_acquire) != FTAR_SLOT_FINALIZED) return;
+    /* it may have reached `seq` (and finalized) since the caller's read: re-read */
+    if (atomic_load_explicit(field, memory_order_acquire) >= seq) return;
+    fprintf(stderr, "ftar: rank %d: rank %d finalized before round %llu (protocol error)\n", job->rank, m,
+            (unsigned long long)seq);
+    ftar_ctrl_abort(job, FTAR_ERR_STATE);
+}
+
 int ftar_ctrl_poll(void *arg)
 {
     ftar_job *job = (ftar_job *)arg;
@@ -215,6 +228,7 @@ static int round_complete(ftar_job *job, uint64_t members, uint64_t seq, double 
         ftar_slot *s = &job->shm->slot[m];
         if (atomic_load_explicit(&s->arrive, memory_order_acquire) >= seq) continue;
         if (ftar_ctrl_is_dead(job, m)) continue;
+        check_finalized(job, m, &s->arrive, seq);
         if (atomic_load_explicit(&s->state, memory_order_acquire) == FTAR_SLOT_EMPTY && now_s() - t0 > 120.0) {
             fprintf(stderr, "ftar: rank %d never joined the job\n", m);
             ftar_ctrl_abort(job, FTAR_ERR_STATE);
@@ -251,18 +265,64 @@ uint64_t ftar_ctrl_agree(ftar_job *job, uint64_t members)
 
 void ftar_ctrl_enter(ftar_job *job)
 {
-    atomic_store_explicit(&job->shm->slot[job->rank].entered, job->seq + 1, memory_order_release);
+    job->xtok = job->seq + 1;
+    atomic_store_explicit(&job->shm->slot[job->rank].entered, job->xtok, memory_order_release);
+}
+
+/* Wait until field `f` of rank m's slot reaches the current exchange token (1) or m is
+ * dead without it (0).  The field is written before the writer can die past it: re-read
+ * after the death test. */
+static int wait_token(ftar_job *job, int m, size_t f)
+{
+    const uint64_t tok = job->xtok;
+    _Atomic uint64_t *v = (_Atomic uint64_t *)((char *)&job->shm->slot[m] + f);
+    for (;;) {
+        if (atomic_load_explicit(v, memory_order_acquire) >= tok) return 1;
+        if (ftar_ctrl_is_dead(job, m)) return atomic_load_explicit(v, memory_order_acquire) >= tok;
+        check_finalized(job, m, v, tok);
+        if (atomic_load_explicit(&job->shm->abort_flag, memory_order_acquire)) exit_aborted(job);
+        cpu_relax();
+    }
 }
 
 int ftar_ctrl_peer_entered(ftar_job *job, int m)
 {
-    const uint64_t tok = job->seq + 1;
-    ftar_slot *s = &job->shm->slot[m];
+    job->xtok = job->seq + 1; /* the caller has entered this exchange itself */
+    return wait_token(job, m, offsetof(ftar_slot, entered));
+}
+
+void ftar_ctrl_launched(ftar_job *job)
+{
+    atomic_store_explicit(&job->shm->slot[job->rank].launched, job->xtok, memory_order_release);
+}
+
+void ftar_ctrl_done(ftar_job *job)
+{
+    atomic_store_explicit(&job->shm->slot[job->rank].done, job->xtok, memory_order_release);
+}
+
+int ftar_ctrl_peer_done(ftar_job *job, int m) { return wait_token(job, m, offsetof(ftar_slot, done)); }
+
+int ftar_ctrl_wait_peers_launched(ftar_job *job, uint64_t members)
+{
+    ftar_shm *S = job->shm;
+    const uint64_t tok = job->xtok;
+    atomic_store_explicit(&S->slot[job->rank].dying, tok, memory_order_release);
     for (;;) {
-        if (atomic_load_explicit(&s->entered, memory_order_acquire) >= tok) return 1;
-        /* entering happens before dying: re-read after the death test */
-        if (ftar_ctrl_is_dead(job, m)) return atomic_load_explicit(&s->entered, memory_order_acquire) >= tok;
-        if (atomic_load_explicit(&job->shm->abort_flag, memory_order_acquire)) exit_aborted(job);
+        int done = 1, launched = 0;
+        for (int m = 0; m < job->size && done; m++) {
+            if (m == job->rank || !(members & (1ull << m))) continue;
+            ftar_slot *s = &S->slot[m];
+            if (atomic_load_explicit(&s->launched, memory_order_acquire) >= tok) {
+                launched++;
+                continue;
+            }
+            if (atomic_load_explicit(&s->arrive, memory_order_acquire) >= tok) continue;
+            if (ftar_ctrl_is_dead(job, m)) continue;
+            done = 0;
+        }
+        if (done) return launched;
+        if (atomic_load_explicit(&S->abort_flag, memory_order_acquire)) exit_aborted(job);
         cpu_relax();
     }
 }

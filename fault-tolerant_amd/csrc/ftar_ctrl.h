@@ -25,7 +25,7 @@
 #include "ftar_dev.h"
 
 #define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
-#define FTAR_SHM_VERSION 2
+#define FTAR_SHM_VERSION 3
 #define FTAR_NBUF 4       /* exported workspace buffers per rank (IN, W, T, R) */
 #define FTAR_DECISIONS 64 /* ring of agree decisions */
 
@@ -59,6 +59,10 @@ typedef struct {
      * point (the agree sequence number is uniform at every step), so a partner decides
      * "the exchange failed" only for a rank that died before entering it */
     _Atomic uint64_t entered;
+    /* the same token once the rank has launched its pulls of the step (or has none), and
+     * once its exchange has completed (its pulls drained: the reference's Sendrecv returned) */
+    _Atomic uint64_t launched;
+    _Atomic uint64_t done;
     /* BARRIER kill point (tests): reached round `dying`'s barrier and will die there */
     _Atomic uint64_t dying;
     char pad[64];
@@ -85,6 +89,7 @@ typedef struct {
     int rank;     /* original rank = slot index */
     int size;
     uint64_t seq; /* agree sequence number */
+    uint64_t xtok; /* exchange token of the step this rank last entered (seq + 1 at entry) */
     int owner;    /* created the segment */
 } ftar_job;
 
@@ -108,6 +113,17 @@ void ftar_ctrl_enter(ftar_job *job);
 /* Wait until original rank m entered the exchange this rank is in (1) or died before
  * entering it (0).  Never returns on abort. */
 int ftar_ctrl_peer_entered(ftar_job *job, int m);
+/* This rank has launched its pulls of the exchange it entered (or has none to launch). */
+void ftar_ctrl_launched(ftar_job *job);
+/* This rank's exchange has completed (its pulls drained). */
+void ftar_ctrl_done(ftar_job *job);
+/* Wait until original rank m completed the exchange this rank is in (1) or died before
+ * completing it (0): the reference's Sendrecv with m failed iff 0. */
+int ftar_ctrl_peer_done(ftar_job *job, int m);
+/* DURING kill point: block until every other member has launched its pulls of the
+ * current exchange, arrived at a later round, or is dead.  Returns how many members had
+ * launched (peers that may be reading this rank's HBM). */
+int ftar_ctrl_wait_peers_launched(ftar_job *job, uint64_t members);
 /* BARRIER kill point: mark this rank as dying at round seq, then block until every
  * other member arrived at round seq, is dead, or is dying at the same round (two victims
  * of one step must not wait for each other). */

@@ -105,6 +105,8 @@ int fdev_order_after(ftar_dev *d, void *user_stream);
 /* Spin (busy, the process stays in R state) until the stream drained.  `poll` is
  * called between queries; a nonzero return aborts the wait with that value. */
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg);
+/* 1 while work queued on the rank's stream has not completed (kill-point diagnostics). */
+int fdev_busy(ftar_dev *d);
 
 int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t bytes);
 int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t bytes);

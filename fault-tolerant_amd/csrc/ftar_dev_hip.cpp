@@ -80,8 +80,6 @@ struct ftar_dev {
         unsigned char handle[FDEV_HANDLE_BYTES];
     } exp[4];
     unsigned long long exp_clock;
-    struct { const void *ptr; size_t bytes; } checked[4]; // device-accessible ranges seen last
-    unsigned checked_next;
 };
 
 extern "C" {
@@ -109,8 +107,6 @@ int fdev_open(int device, ftar_dev **out)
     d->profiling = 0;
     memset(d->exp, 0, sizeof(d->exp));
     d->exp_clock = 0;
-    memset(d->checked, 0, sizeof(d->checked));
-    d->checked_next = 0;
     memset(&d->ctr, 0, sizeof(d->ctr));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -252,8 +248,8 @@ int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, 
 
 int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes)
 {
-    for (auto &k : d->checked)
-        if (k.ptr == ptr && bytes <= k.bytes) return 0;
+    // one attribute query per buffer and call: a cache keyed on the address would also
+    // accept a freed-and-reallocated smaller block at the same address
     hipPointerAttribute_t a;
     memset(&a, 0, sizeof(a));
     if (hipPointerGetAttributes(&a, ptr) != hipSuccess) {
@@ -261,8 +257,9 @@ int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes)
         return 1; // not memory the runtime knows (pageable host memory)
     }
     if (a.type == hipMemoryTypeUnregistered) return 1;
-    if (a.type == hipMemoryTypeDevice) { // the whole range inside one allocation
-        hipDeviceptr_t base = nullptr;
+    if (a.type == hipMemoryTypeDevice) {
+        if (a.device != d->device) return 1; // another GPU's memory: the kernels run on ours
+        hipDeviceptr_t base = nullptr;     // the whole range inside one allocation
         size_t size = 0;
         if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
             (void)hipGetLastError();
@@ -270,9 +267,6 @@ int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes)
         }
         if ((size_t)((const char *)ptr - (const char *)base) + bytes > size) return 1;
     }
-    d->checked[d->checked_next].ptr = ptr;
-    d->checked[d->checked_next].bytes = bytes;
-    d->checked_next = (d->checked_next + 1) % 4;
     return 0;
 }
 
@@ -535,6 +529,14 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
     int rc = sync_stream(d, d->stream, poll, arg);
     if (rc) return rc;
     return harvest(d);
+}
+
+int fdev_busy(ftar_dev *d)
+{
+    hipError_t e = hipStreamQuery(d->stream);
+    if (e == hipErrorNotReady) return 1;
+    if (e != hipSuccess) (void)hipGetLastError();
+    return 0;
 }
 
 int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg)

@@ -74,6 +74,7 @@ struct ftar_comm {
 
     int profiling;
     ftar_stats stats;
+    int chunk_cont; /* the host pipeline's chunks 2..n of one user call (see ftar_stats_begin) */
     int verbose;
     int overlap;         /* FTAR_OVERLAP (default 1): Raben step-0 redundancy copy on the background stream */
     int relay;           /* FTAR_RELAY (default 1): stripe exchanges over 2-hop paths */
@@ -89,6 +90,8 @@ size_t ftar_esize(int dtype);
 int ftar_my_comm_rank(const ftar_comm *c);
 int ftar_comm_rank_of(const ftar_comm *c, int w);
 
+/* collective: grow the _host entry points' staging to `bytes` (aborts the job on failure) */
+int ftar_ensure_staging(ftar_comm *c, size_t bytes);
 /* collective: grow the exported workspace to hold `bytes` per buffer */
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes);
 /* pointer to buffer b of original rank w (own or peer mapping) */
@@ -126,6 +129,14 @@ int ftar_is_dead(ftar_comm *c, int w);
  * death is noticed (a rank that dies after its exchange point is still read). */
 void ftar_enter(ftar_comm *c);
 int ftar_peer_entered(ftar_comm *c, int w);
+/* After this rank has queued its pulls of the step it entered (before draining them):
+ * publish that, then pass the FTAR_PT_DURING kill point of (phase, step). */
+void ftar_launched(ftar_comm *c, int phase, int step);
+/* After the step's pulls drained: this rank's side of the exchange completed. */
+void ftar_exchange_done(ftar_comm *c);
+/* The reference's Sendrecv with original rank w failed (0) iff w died before completing
+ * its side of the exchange -- mid-transfer included (FTAR_PT_DURING). */
+int ftar_peer_done(ftar_comm *c, int w);
 
 /* deterministic fault injection at (phase, step, point) */
 void ftar_maybe_die(ftar_comm *c, int phase, int step, int point);

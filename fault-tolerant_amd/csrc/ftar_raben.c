@@ -283,6 +283,7 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
 
     /* reduce-scatter: T(v, L) over this rank's final block */
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BEFORE);
+    ftar_enter(c);
     const void *src[FDEV_MAX_TREE];
     unsigned remote = 0;
     for (int j = 0; j < p; j++) {
@@ -296,8 +297,11 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
+    ftar_launched(c, FTAR_PH_LOOP, 0); /* every step's DURING point: the one launch is in flight */
+    for (int s = 1; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_DURING);
     ftar_drain(c);
-    c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
+    ftar_exchange_done(c);
+    c->stats.step0_link_bytes += ftar_link_bytes(c) - lb0;
     c->stats.steps += L;
     c->stats.mesh_steps++;
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_AFTER);
@@ -307,6 +311,7 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
 
     /* allgather: every peer's final block into rbuf, this rank's own out of W */
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
+    ftar_enter(c);
     fdev_seg segs[FDEV_MAX_SEGS];
     int ns = 0;
     segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, own0), at(x, W, own0), NULL, (size_t)own_n, NULL};
@@ -319,7 +324,10 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
                                 (size_t)rc[L - 1], NULL};
     }
     ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
+    ftar_launched(c, FTAR_PH_AG, L - 1);
+    for (int s = L - 2; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_DURING);
     ftar_drain(c);
+    ftar_exchange_done(c);
     c->stats.steps += L;
     c->stats.mesh_steps++;
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_AFTER);
@@ -329,6 +337,7 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
 
     /* ERRORS_ARE_FATAL barrier (:357-360); no post-step at rem = 0 */
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
     ftar_sync_fatal(c);
@@ -348,6 +357,7 @@ static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
     ftar_comm *c = x->c;
     const int L = x->steps, p = x->adjsize, v = x->vrank;
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BEFORE);
+    ftar_enter(c);
     const void *src[FDEV_MAX_BATCH * FDEV_MAX_BATCH];
     void *out[FDEV_MAX_BATCH];
     size_t n[FDEV_MAX_BATCH];
@@ -374,8 +384,11 @@ static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
+    ftar_launched(c, FTAR_PH_LOOP, 0);
+    for (int s = 1; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_DURING);
     ftar_drain(c);
-    c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
+    ftar_exchange_done(c);
+    c->stats.step0_link_bytes += ftar_link_bytes(c) - lb0;
     c->stats.steps += 2 * L;
     c->stats.mesh_steps++;
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_AFTER);
@@ -383,11 +396,16 @@ static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
     uint64_t newf = ftar_step_sync(c, 2); /* agree + barrier (:258-265) */
     if (newf) rb_handler_rs(x, newf, L - 1); /* no idle rank: aborts */
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
+    ftar_enter(c); /* the allgather's data already moved in the one launch */
+    ftar_launched(c, FTAR_PH_AG, L - 1);
+    for (int s = L - 2; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_DURING);
+    ftar_exchange_done(c);
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_AFTER);
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BARRIER);
     newf = ftar_step_sync(c, 2); /* (:330-335) */
     if (newf) rb_handler_ag(x, newf, 0); /* no idle rank: aborts */
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
     ftar_sync_fatal(c);
@@ -482,6 +500,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     /* ---- pre-step (:61-139): failures are fatal here ---- */
     ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BEFORE);
     if (x->fast_io) {
+        ftar_enter(c);
+        ftar_launched(c, FTAR_PH_PRE, 0);
+        ftar_exchange_done(c);
         ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
         ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
         ftar_sync_fatal(c); /* every IN is ready; the barrier before the tolerant region (:166) */
@@ -489,8 +510,10 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     } else {
         ftar_sync_fatal(c); /* every IN is ready */
         ftar_resolve_inputs(c);
+        ftar_enter(c);
         int64_t lh = (int64_t)count / 2, rh = (int64_t)count - lh;
-        if (x->rank < 2 * x->rem) {
+        int pair = x->rank < 2 * x->rem;
+        if (pair) {
             if (x->rank % 2 != 0) { /* odd: reduce the right half with the even's right half */
                 void *P = ftar_buf(c, c->order[x->rank - 1], WS_IN);
                 run_reduce(x, at(x, IN, lh), at(x, IN, lh), at(x, P, lh), rh, FDEV_REMOTE_Y, FDEV_TAG_STEP);
@@ -498,9 +521,13 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                 void *P = ftar_buf(c, c->order[x->rank + 1], WS_IN);
                 run_reduce(x, IN, IN, P, lh, FDEV_REMOTE_Y, FDEV_TAG_STEP);
             }
+        }
+        ftar_launched(c, FTAR_PH_PRE, 0);
+        if (pair) {
             ftar_drain(c);
             c->stats.steps++;
         }
+        ftar_exchange_done(c);
         ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
         ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
         ftar_sync_fatal(c);
@@ -526,12 +553,20 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         rb_plan(x, step, mask, 0, &P);
         ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BEFORE);
         ftar_enter(c);
-        int skip = 0;
+        int skip = 0, pw = -1;
         if (x->vrank != -1) {
-            int pw = c->order[rb_real(x, x->vrank ^ mask)];
+            pw = c->order[rb_real(x, x->vrank ^ mask)];
             if (!ftar_peer_entered(c, pw)) skip = x->corr = 1; /* the exchange failed (:238-241) */
             c->stats.steps++;
         }
+        /* A partner that dies mid-exchange (after entering, before its side completed) fails
+         * the Sendrecv too: the reference then discards the received window (corr, :238-241)
+         * and the RS handler rebuilds it from the impersonator's replay.  The pull reduces in
+         * place, so while a recovery is possible (an idle rank exists; at step 0 the handler
+         * aborts) the window's pre-image is kept in T -- whose half rw0 is unused (T holds
+         * the partner's other half, sw0) -- to undo the reduce. */
+        int guard = x->rem > 0 && step >= 1 && pw >= 0 && !skip;
+        if (guard) run_copy(x, at(x, T, x->rindex[step]), at(x, W, x->rindex[step]), x->rcount[step], 0, FDEV_TAG_LOCAL);
         double lb0 = ftar_link_bytes(c);
         int tag = step == 0 ? FDEV_TAG_STEP0 : FDEV_TAG_STEP;
         if (step == 0 && c->overlap && !ftar_xfer_would_relay(c, &P, x->es)) {
@@ -553,13 +588,24 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                     ftar_run_pulls(c, x->dtype, x->op, &s1, 1, FDEV_TAG_BG, 1);
                     x->bg_pending = 1;
                 }
-                ftar_drain(c);
             }
+            ftar_launched(c, FTAR_PH_LOOP, step);
+            if (x->vrank != -1 && !skip) ftar_drain(c);
+            ftar_exchange_done(c);
             ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_AFTER);
         } else {
             ftar_xfer_step(c, &P, x->dtype, x->op, tag, skip, FTAR_PH_LOOP, step, NULL, 0, &xs);
         }
-        if (step == 0) c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
+        if (guard && !ftar_peer_done(c, pw)) { /* partner died mid-exchange: corr */
+            run_copy(x, at(x, W, x->rindex[step]), at(x, T, x->rindex[step]), x->rcount[step], 0, FDEV_TAG_RECOV);
+            ftar_drain(c);
+            x->corr = 1;
+            xs.skipped = 1; /* nothing of this window is re-pulled after the agree */
+            if (c->verbose)
+                fprintf(stderr, "ftar: rank %d: partner %d died mid-exchange at RS step %d: window discarded\n",
+                        c->wrank, pw, step);
+        }
+        if (step == 0) c->stats.step0_link_bytes += ftar_link_bytes(c) - lb0;
         ftar_maybe_die(c, FTAR_PH_LOOP, step, FTAR_PT_BARRIER);
         uint64_t newf = ftar_step_sync(c, 2 * x->steps); /* agree + barrier (:258-265) */
         if (newf) {
@@ -607,6 +653,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
 
     /* ---- ERRORS_ARE_FATAL barrier + post-step (:357-381) ---- */
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
     ftar_sync_fatal(c);
@@ -634,14 +681,7 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
     size_t es = ftar_esize(dtype);
     if (es == 0) return FTAR_ERR_ARG;
     size_t bytes = count * es;
-    if (bytes > c->hbytes) {
-        fdev_free(c->dev, c->hsend);
-        fdev_free(c->dev, c->hrecv);
-        c->hsend = c->hrecv = NULL;
-        if (fdev_alloc_plain(c->dev, bytes, &c->hsend) || fdev_alloc_plain(c->dev, bytes, &c->hrecv))
-            return FTAR_ERR_NOMEM;
-        c->hbytes = bytes;
-    }
+    ftar_ensure_staging(c, bytes);
     /* Power of two without a spare (every failure aborts, so nothing is recovered across
      * calls): the vector goes through as a pipeline of chunk Allreduces -- chunk k's
      * H2D, chunk k-1's Allreduce and chunk k-2's D2H in flight at once (copy engines both
@@ -678,8 +718,10 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
     for (size_t off = 0; off < count; off += per, n++) {
         size_t m = count - off < per ? count - off : per;
         if (fdev_wait_h2d(c->dev, n, ftar_ctrl_poll, &c->job)) return FTAR_ERR_DEVICE;
+        c->chunk_cont = n > 0;
         int rc = ftar_allreduce_rabenseifner((char *)c->hsend + off * es, (char *)c->hrecv + off * es, m, dtype, op,
                                              c);
+        c->chunk_cont = 0;
         if (rc) return rc;
         if (fdev_d2h_async(c->dev, (char *)rbuf + off * es, (char *)c->hrecv + off * es, m * es))
             return FTAR_ERR_DEVICE;

@@ -211,15 +211,21 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     uint64_t newf = ftar_sync(c); /* every IN is ready */
     if (newf & involved) ftar_abort(c, FTAR_ERR_PROC_FAILED);
     ftar_resolve_inputs(c);
+    ftar_enter(c);
     int ia = index_of(x->active, x->nactive, me);
-    if (ia >= 0 && ia < x->ninactive) {
+    int pre = ia >= 0 && ia < x->ninactive;
+    if (pre) {
         const void *P = ftar_buf(c, x->inactive[ia], WS_IN);
         run1(x, FDEV_REDUCE, c->ws[WS_W], ftar_local(c, WS_IN), P, FDEV_REMOTE_Y, FDEV_TAG_STEP); /* src = dst + src */
+    }
+    ftar_launched(c, FTAR_PH_PRE, 0);
+    if (pre) {
         ftar_drain(c);
         x->cur = WS_W;
         publish_cur(x);
         c->stats.steps++;
     }
+    ftar_exchange_done(c);
     ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
     ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
     newf = ftar_sync(c); /* MPI_Barrier after switching to ERRORS_RETURN (:16-18) */
@@ -259,7 +265,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
         double lb0 = ftar_link_bytes(c);
         ftar_xfer_step(c, &P, x->dtype, x->op, iter == 0 ? FDEV_TAG_STEP0 : FDEV_TAG_STEP, skip, FTAR_PH_LOOP, iter,
                        NULL, 0, &xs);
-        if (iter == 0) c->stats.step0_link_bytes = ftar_link_bytes(c) - lb0;
+        if (iter == 0) c->stats.step0_link_bytes += ftar_link_bytes(c) - lb0;
         if (i >= 0 && !skip) {
             x->cur = out;
             publish_cur(x);
@@ -276,6 +282,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
 
     /* ERRORS_ARE_FATAL barrier (:73-75), then the fan-out to inactive ranks (:78-89) */
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
     ftar_sync_fatal(c);
@@ -301,14 +308,7 @@ int ftar_recursive_doubling_host(const void *src, void *dst, size_t count, ftar_
     size_t es = ftar_esize(dtype);
     if (es == 0) return FTAR_ERR_ARG;
     size_t bytes = count * es;
-    if (bytes > c->hbytes) {
-        fdev_free(c->dev, c->hsend);
-        fdev_free(c->dev, c->hrecv);
-        c->hsend = c->hrecv = NULL;
-        if (fdev_alloc_plain(c->dev, bytes, &c->hsend) || fdev_alloc_plain(c->dev, bytes, &c->hrecv))
-            return FTAR_ERR_NOMEM;
-        c->hbytes = bytes;
-    }
+    ftar_ensure_staging(c, bytes);
     if (bytes && fdev_h2d(c->dev, c->hsend, src, bytes)) return FTAR_ERR_DEVICE;
     int rc = ftar_recursive_doubling(c->hsend, c->hrecv, count, dtype, op, c);
     if (rc) return rc;

@@ -213,10 +213,10 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
                 const ftar_pull *pl = &p->pull[me][u];
                 segs[ns++] = own_seg(c, pl, pl->off, pl->n, at(ftar_buf(c, pl->src, pl->src_buf), pl->off, es), es);
             }
-        if (ns) {
-            ftar_run_pulls(c, dtype, op, segs, ns, tag, 0);
-            ftar_drain(c);
-        }
+        if (ns) ftar_run_pulls(c, dtype, op, segs, ns, tag, 0);
+        ftar_launched(c, kphase, kstep); /* FTAR_PT_DURING: our pulls and the partner's in flight */
+        if (ns) ftar_drain(c);
+        ftar_exchange_done(c);
         ftar_maybe_die(c, kphase, kstep, FTAR_PT_AFTER);
         return;
     }
@@ -258,10 +258,12 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
             segs[ns++] = s;
         }
     }
-    if (ns) {
-        ftar_run(c, dtype, op, segs, ns, tag);
-        ftar_drain(c);
-    }
+    if (ns) ftar_run(c, dtype, op, segs, ns, tag);
+    ftar_launched(c, kphase, kstep); /* FTAR_PT_DURING: phase-1 pulls (ours and the relays') in flight */
+    if (ns) ftar_drain(c);
+    /* this rank's side of the exchange is complete once its phase 1 drained: a death
+     * after this point (AFTER) leaves the partner's exchange intact, as in the direct form */
+    ftar_exchange_done(c);
     ftar_maybe_die(c, kphase, kstep, FTAR_PT_AFTER);
     /* mid-step barrier: relays that died before finishing phase 1 are known to all */
     xs->mid_dead = ftar_sync(c);

@@ -23,7 +23,9 @@ else
     KILL=$((RANDOM % (N - 1) + 1))
 fi
 export FTAR_LOOP_SECONDS=${FTAR_LOOP_SECONDS:-4}
-timeout "$TIMEOUT" ../bin/ftrun -np $N ./$EXE_PATH $BUF_SIZE > ../out/mpi_out.txt &
+# The program goes through FTAR_PROG, so neither `timeout` nor the launcher has "main" on
+# its command line: the killer's candidates (kill_procs.sh) are the rank processes only.
+FTAR_PROG=./$EXE_PATH timeout "$TIMEOUT" ../bin/ftrun -np $N $BUF_SIZE > ../out/mpi_out.txt &
 # FTAR_KILLER swaps the killer (e.g. one that only targets this job's ranks, whose
 # launcher pid is exported as FTAR_JOB_PID); the default is the reference's.
 FTAR_JOB_PID=$! ${FTAR_KILLER:-./kill_procs.sh} "$DELAY" "$KILL" > ../out/docker_out.txt &

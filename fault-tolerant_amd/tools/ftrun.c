@@ -3,17 +3,22 @@
  *          `mpiexec --with-ft ulfm -np N ./main BUF` (reference run/run_mpi.sh:24-26).
  *
  *   ftrun -np N [--devmap d0,d1,...] [--] prog [args...]
+ *   FTAR_PROG=prog ftrun -np N [--devmap ...] [--] [args...]
+ *
+ * With FTAR_PROG the program path is not on the launcher's command line, so the
+ * harness's killer (kill_procs.sh: R-state processes whose command line contains
+ * "main", run/kill_procs.sh:12) can never pick the launcher: the ranks run `prog args`.
  *
  * FTAR_PIN_CPUS=1 pins rank r to the r-th CPU of the launcher's affinity set (CPU
  * baseline runs of the host-memory build: one process per core).
  *
  * Creates the job's shared-memory control block, starts N rank processes (one per
  * GPU by default: rank r drives device r % ngpus, or devmap[r]), and reaps them.
- * The launcher itself never touches the GPU and sleeps in waitpid, so the harness's
- * kill_procs.sh (which only shoots R-state processes whose command line contains
- * "main", run/kill_procs.sh:12) never picks it.  A rank that dies is detected by its
- * peers through the control block; the launcher only reaps, forwards MPI_Abort to
- * every remaining rank, and cleans up on SIGTERM (run_mpi.sh's `timeout 30`).
+ * The launcher itself never touches the GPU and sleeps in sigtimedwait (S state) until a
+ * rank exits or a signal arrives.  A rank that dies is detected by its peers through the
+ * control block; the launcher only reaps, forwards MPI_Abort to every remaining rank
+ * (checked whenever it wakes, at least every 50 ms), and cleans up on SIGTERM
+ * (run_mpi.sh's `timeout 30`).
  */
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
@@ -35,13 +40,7 @@
 static pid_t g_pids[FTAR_MAX_RANKS];
 static int g_n;
 static char g_name[128];
-static volatile sig_atomic_t g_term;
-
-static void on_term(int sig)
-{
-    (void)sig;
-    g_term = 1;
-}
+static int g_term;
 
 static void kill_all(void)
 {
@@ -51,7 +50,8 @@ static void kill_all(void)
 
 static void usage(void)
 {
-    fprintf(stderr, "usage: ftrun -np N [--devmap d0,d1,...] [--] prog [args...]\n");
+    fprintf(stderr, "usage: ftrun -np N [--devmap d0,d1,...] [--] prog [args...]\n"
+                    "       FTAR_PROG=prog ftrun -np N [--devmap d0,d1,...] [--] [args...]\n");
     exit(2);
 }
 
@@ -73,7 +73,15 @@ int main(int argc, char **argv)
             break;
         }
     }
-    if (np < 1 || np > FTAR_MAX_RANKS || ai >= argc) usage();
+    const char *prog = getenv("FTAR_PROG");
+    if (prog && !*prog) prog = NULL;
+    if (np < 1 || np > FTAR_MAX_RANKS || (!prog && ai >= argc)) usage();
+    /* the ranks' argv: prog (FTAR_PROG or the first argument) + the remaining arguments */
+    int rest = prog ? ai : ai + 1;
+    char **rargv = calloc((size_t)(argc - rest + 2), sizeof(char *));
+    if (!rargv) return 1;
+    rargv[0] = (char *)(prog ? prog : argv[ai]);
+    for (int i = rest; i < argc; i++) rargv[1 + i - rest] = argv[i];
     g_n = np;
     snprintf(g_name, sizeof(g_name), "/ftar-job-%d", (int)getpid());
     ftar_job job;
@@ -94,11 +102,14 @@ int main(int argc, char **argv)
         }
     }
 
-    struct sigaction sa;
-    memset(&sa, 0, sizeof(sa));
-    sa.sa_handler = on_term;
-    sigaction(SIGTERM, &sa, NULL);
-    sigaction(SIGINT, &sa, NULL);
+    /* SIGCHLD / SIGTERM / SIGINT are taken synchronously by sigtimedwait below; the
+     * children get the default mask and dispositions back before exec */
+    sigset_t wset, oldset;
+    sigemptyset(&wset);
+    sigaddset(&wset, SIGCHLD);
+    sigaddset(&wset, SIGTERM);
+    sigaddset(&wset, SIGINT);
+    sigprocmask(SIG_BLOCK, &wset, &oldset);
 
     pid_t parent = getpid();
     for (int r = 0; r < np; r++) {
@@ -110,8 +121,10 @@ int main(int argc, char **argv)
             return 1;
         }
         if (pid == 0) {
+            sigprocmask(SIG_SETMASK, &oldset, NULL);
             prctl(PR_SET_PDEATHSIG, SIGKILL);
             if (getppid() != parent) _exit(1);
+            unsetenv("FTAR_PROG");
             char buf[32];
             setenv("FTAR_JOB", g_name, 1);
             snprintf(buf, sizeof(buf), "%d", r);
@@ -139,8 +152,8 @@ int main(int argc, char **argv)
                     }
                 }
             }
-            execvp(argv[ai], &argv[ai]);
-            fprintf(stderr, "ftrun: exec %s: %s\n", argv[ai], strerror(errno));
+            execvp(rargv[0], rargv);
+            fprintf(stderr, "ftrun: exec %s: %s\n", rargv[0], strerror(errno));
             _exit(127);
         }
         g_pids[r] = pid;
@@ -151,6 +164,12 @@ int main(int argc, char **argv)
     while (alive > 0) {
         int st;
         pid_t p = waitpid(-1, &st, WNOHANG);
+        if (p == 0) { /* nothing to reap: sleep until a child exits, a signal, or 50 ms */
+            struct timespec tmo = {0, 50 * 1000 * 1000};
+            int sig = sigtimedwait(&wset, NULL, &tmo);
+            if (sig == SIGTERM || sig == SIGINT) g_term = 1;
+            p = waitpid(-1, &st, WNOHANG);
+        }
         if (p > 0) {
             for (int r = 0; r < np; r++)
                 if (g_pids[r] == p) g_pids[r] = -1;
@@ -173,8 +192,6 @@ int main(int argc, char **argv)
             kill_all();
             abort_forwarded = 1;
         }
-        struct timespec ts = {0, 1000 * 1000};
-        nanosleep(&ts, NULL);
     }
     int aborted = atomic_load(&job.shm->abort_flag);
     int code = aborted ? atomic_load(&job.shm->abort_code) : exit_code;

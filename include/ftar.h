@@ -71,6 +71,12 @@ typedef enum {
  *   FTAR_PT_AFTER    exchange done, dies before its local reduce / before arriving at the barrier
  *   FTAR_PT_BARRIER  completes the step, waits until every peer arrived, then dies (no peer ever
  *                    touches its memory while it dies)
+ *   FTAR_PT_DURING   mid-exchange: has entered the step and launched its own pull kernel, waits
+ *                    until every peer has launched its pulls of the step (some read this rank's
+ *                    HBM), then dies with its kernel in flight.  Like a Sendrecv that fails
+ *                    mid-transfer in the reference (raben/rabenseifner.c:209-211, 238-241), the
+ *                    partner's exchange of that step counts as failed (`corr`): the window it
+ *                    pulled is discarded and rebuilt by the error handler.
  */
 #define FTAR_PH_PRE  0
 #define FTAR_PH_LOOP 1
@@ -80,6 +86,7 @@ typedef enum {
 #define FTAR_PT_BEFORE  0
 #define FTAR_PT_AFTER   1
 #define FTAR_PT_BARRIER 2
+#define FTAR_PT_DURING  3
 
 typedef struct {
     int rank;  /* original world rank of the victim */

@@ -128,6 +128,12 @@ static void poison(sim_t *s, void *buf, size_t n)
     }
 }
 
+/* A partner's Sendrecv with a rank that dies at kill point `kp` of the step failed: the
+ * rank died before its exchange (BEFORE) or in the middle of it (DURING, a transfer cut
+ * short: raben/rabenseifner.c:209-211 return an error, :238-241 mark corr).  A rank that
+ * dies after its Sendrecv returned (AFTER, BARRIER) had delivered its data. */
+static int failed_xchg(int kp) { return kp == FTAR_PT_BEFORE || kp == FTAR_PT_DURING; }
+
 /* Does original rank w die at (phase, step)?  Returns the point or -1. */
 static int kill_point(const sim_t *s, int w, int phase, int step)
 {
@@ -465,7 +471,7 @@ int ftar_oracle_rabenseifner(int p, size_t count, int dtype, int op, const void 
             if (dest_of[c] < 0 || kp[w] == FTAR_PT_BEFORE) continue;
             int dw = B.order[dest_of[c]];
             rb_rank *d = &B.rk[dw];
-            if (kp[dw] == FTAR_PT_BEFORE) { /* partner died before sending: :238-241 */
+            if (failed_xchg(kp[dw])) { /* partner died before or during its Sendrecv: :238-241 */
                 r->corr = 1;
                 poison(&S, ELEM(r->tmp, (size_t)r->rindex[step], es), (size_t)r->rcount[step]);
                 continue;
@@ -481,7 +487,7 @@ int ftar_oracle_rabenseifner(int p, size_t count, int dtype, int op, const void 
             int w = B.order[c];
             rb_rank *r = &B.rk[w];
             if (dest_of[c] < 0) continue;
-            if (got[c] && kp[w] != FTAR_PT_AFTER && kp[w] != FTAR_PT_BEFORE)
+            if (got[c] && kp[w] != FTAR_PT_AFTER && kp[w] != FTAR_PT_BEFORE && kp[w] != FTAR_PT_DURING)
                 reduce_into(&S, ELEM(r->rbuf, (size_t)r->rindex[step], es), ELEM(r->tmp, (size_t)r->rindex[step], es),
                             (size_t)r->rcount[step]);
             if (step + 1 < B.steps) { /* :244-249 */
@@ -518,7 +524,7 @@ int ftar_oracle_rabenseifner(int p, size_t count, int dtype, int op, const void 
             int dw = B.order[dest];
             rb_rank *d = &B.rk[dw];
             stage[c] = (unsigned char *)malloc((size_t)r->scount[step] * es + 1);
-            if (kp[dw] == FTAR_PT_BEFORE) {
+            if (failed_xchg(kp[dw])) {
                 poison(&S, stage[c], (size_t)r->scount[step]);
             } else {
                 memcpy(stage[c], ELEM(d->rbuf, (size_t)d->rindex[step], es), (size_t)r->scount[step] * es);
@@ -792,7 +798,7 @@ int ftar_oracle_recursive_doubling(int p, size_t count, int dtype, int op, const
             if (kp[w] == FTAR_PT_BEFORE || (!B.rk[w].alive && kp[w] < 0)) continue;
             int pw = B.active[i ^ distance];
             stage[i] = (unsigned char *)malloc(count * es + 1);
-            if (kp[pw] == FTAR_PT_BEFORE || (!B.rk[pw].alive && kp[pw] < 0))
+            if (failed_xchg(kp[pw]) || (!B.rk[pw].alive && kp[pw] < 0))
                 poison(&S, stage[i], count); /* Sendrecv error ignored (:35-37): corrupted */
             else
                 memcpy(stage[i], B.rk[pw].src, count * es);
@@ -802,7 +808,7 @@ int ftar_oracle_recursive_doubling(int p, size_t count, int dtype, int op, const
             rd_rank *r = &B.rk[B.active[i]];
             memcpy(r->dst, stage[i], count * es);
             free(stage[i]);
-            if (kp[B.active[i]] == FTAR_PT_AFTER) continue;
+            if (kp[B.active[i]] == FTAR_PT_AFTER || kp[B.active[i]] == FTAR_PT_DURING) continue;
             if (last) reduce_into(&S, r->dst, r->src, count); /* :44 Reduce_local(src, dst) */
             else reduce_into(&S, r->src, r->dst, count);      /* :48 Reduce_local(dst, src) */
         }

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "_build", "libftar_oracle.so")
 INT32, FLOAT32, INT64, FLOAT64 = 0, 1, 2, 3
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
 PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
-PT_BEFORE, PT_AFTER, PT_BARRIER = 0, 1, 2
+PT_BEFORE, PT_AFTER, PT_BARRIER, PT_DURING = 0, 1, 2, 3
 OK, DEAD, ABORTED = 0, 1, 2
 MAX_RANKS = 64
 

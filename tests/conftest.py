@@ -14,6 +14,27 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: longer multi-process runs")
+    # FTAR_HEARTBEAT=<file>: a line every 20 s naming the running test, so a long
+    # full-size case is not mistaken for a hang by a watchdog that watches output files
+    path = os.environ.get("FTAR_HEARTBEAT")
+    if path:
+        import threading
+        import time
+
+        def beat():
+            while True:
+                with open(path, "a") as f:
+                    f.write(f"{time.strftime('%H:%M:%S')} {_current[0]}\n")
+                time.sleep(20)
+
+        threading.Thread(target=beat, daemon=True).start()
+
+
+_current = ["(collecting)"]
+
+
+def pytest_runtest_logstart(nodeid, location):
+    _current[0] = nodeid
 
 
 def load_package():

@@ -97,6 +97,15 @@ int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
  * shared-memory objects too, so they can be exported like hipMalloc memory */
 int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr)
 {
+    /* FTAR_HOSTSIM_FAIL_PLAIN=k: the k-th staging allocation (1-based) of rank
+     * FTAR_HOSTSIM_FAIL_RANK (default 0) fails, as hipMalloc out of memory would */
+    static int nplain;
+    const char *k = getenv("FTAR_HOSTSIM_FAIL_PLAIN"), *fr = getenv("FTAR_HOSTSIM_FAIL_RANK");
+    const char *me = getenv("FTAR_RANK");
+    if (k && ++nplain == atoi(k) && me && atoi(me) == (fr ? atoi(fr) : 0)) {
+        snprintf(g_err, sizeof(g_err), "injected staging allocation failure");
+        return 102;
+    }
     unsigned char h[FDEV_HANDLE_BYTES];
     return fdev_alloc_shared(d, bytes ? bytes : 1, ptr, h);
 }
@@ -275,6 +284,8 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
     if (poll) return poll(arg);
     return 0;
 }
+
+int fdev_busy(ftar_dev *d) { return 0; } /* host "kernels" complete at launch */
 
 int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t n)
 {

@@ -1,0 +1,146 @@
+"""Kills with data in flight, and the BASELINE configs at their full size, on the GPU.
+
+FTAR_PT_DURING (include/ftar.h): the victim has entered the step, launched its own pull
+kernel, waited until every peer launched its pulls of the step (its partner's kernel
+reads the victim's HBM), and is SIGKILLed with its kernel still queued or running.  The
+reference's counterpart is a Sendrecv cut short by the death
+(/root/reference/src/raben/rabenseifner.c:209-211 returns an error, :238-241 marks the
+received window `corr`): the partner discards what it pulled and the error handler
+rebuilds the window (raben/errhandler.c:159-181).  The oracle models exactly that, so
+survivors must match it bit for bit -- with MAX over NaN / signed zeros the operand
+order of the rebuilt window shows that the `corr` path ran.
+
+Full size: BASELINE.json configs[2..4] are 256 MiB of float32 per rank at p = 8 (and
+C5: p = 9 = 8 + one idle spare, a kill mid-exchange).  Every rank of these jobs shares
+the one GPU of the test box, so the fabric is local HBM; the schedules, IPC mappings,
+control plane and recovery are the ones the 8-GPU node runs.
+"""
+import numpy as np
+import pytest
+
+import harness as H
+
+pytestmark = pytest.mark.gpu
+
+ALL_ON_GPU0 = ",".join(["0"] * 16)
+FULL = 1 << 26  # 64 Mi float32 = 256 MiB per rank
+RELAY_ALL = {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}
+REFERENCE_SHAPE = {"FTAR_MESH": "0", "FTAR_REDUNDANCY": "1", "FTAR_OVERLAP": "0", "FTAR_RELAY": "0"}
+
+
+def _check(fn, algo, inputs, kills=(), op=0, env=None, timeout=300):
+    o = fn(inputs, kills, op=op)
+    r = H.run_probe(algo, inputs, kills, op=op, backend="gpu", devmap=ALL_ON_GPU0, timeout=timeout,
+                    env_extra=env)
+    u = {4: np.uint32, 8: np.uint64}[inputs[0].dtype.itemsize]
+    if o.aborted:
+        assert r.aborted, r.stderr[-2000:]
+        assert not r.outputs
+        return o, r
+    assert not r.aborted, r.stderr[-2000:]
+    assert r.returncode == 0, r.stderr[-2000:]
+    for w, st in enumerate(o.status):
+        if st == 0:
+            assert w in r.outputs, (w, r.stderr[-2000:])
+            assert np.array_equal(r.outputs[w][0].view(u), o.outputs[w].view(u)), (w, algo, kills)
+        else:
+            assert w not in r.outputs
+    return o, r
+
+
+def _died_mid_exchange(r, victim):
+    """The victim's own line: 'rank V dies mid-exchange (...): own kernel X, N peers launched'."""
+    for line in r.stderr.splitlines():
+        if f"rank {victim} dies mid-exchange" in line:
+            t = line.split(":")[-1].split(",")
+            return "in flight" in t[0], int(t[1].split()[0])
+    raise AssertionError(f"no mid-exchange death of rank {victim}: {r.stderr[-2000:]}")
+
+
+# C5 layout: 9 ranks = 8 + idle spare (rank 1 pairs with rank 0 in the pre-step); the
+# victim original rank 6 is vrank 5
+@pytest.mark.parametrize("kill", [(6, 1, 1, 3), (6, 2, 1, 3), (3, 1, 2, 3), (8, 2, 0, 3), (6, 1, 0, 3),
+                                  (6, 2, 2, 3), (0, 1, 1, 3), (1, 1, 1, 3)])
+def test_during_kill_p9(oracle, kill):
+    """RS step 1 / AG step 1 / RS step 2 / last AG step recover (new_entry = the spare);
+    RS step 0 and the first AG step abort (raben/errhandler.c:37-38, 320-323); the
+    spare's partner and the idle spare itself die mid-exchange."""
+    o, r = _check(oracle.rabenseifner, "raben", oracle.random_inputs(9, (1 << 20) + 5, seed=90 + kill[0]), [kill])
+    if not o.aborted:
+        assert r.status and all(st[0][3] == 1 for w, st in r.status.items()), r.status  # one recovery
+    _died_mid_exchange(r, kill[0])
+
+
+@pytest.mark.parametrize("kill", [(3, 1, 1, 3), (2, 1, 1, 3), (4, 1, 1, 3)])
+def test_during_kill_p5_operand_order(oracle, kill):
+    """p = 5 (4 + one idle spare), MAX over NaN / signed zeros / infinities: the partner's
+    window must be the handler's rebuild (impersonator's operand order), not the pull."""
+    ins = H.with_specials(oracle.random_inputs(5, 65536 + 5, seed=500 + kill[0]), 11)
+    o = oracle.rabenseifner(ins, [kill], op=2)
+    assert not o.aborted and o.status[kill[0]] == oracle.DEAD
+    _check(oracle.rabenseifner, "raben", ins, [kill], op=2)
+
+
+@pytest.mark.parametrize("form", ["0", str(1 << 20)])
+@pytest.mark.parametrize("kill", [(3, 1, 1, 3), (5, 2, 0, 3), (0, 1, 2, 3)])
+def test_during_kill_mesh_p8_aborts(oracle, kill, form):
+    """p = 8, no idle rank: the one-hop mesh (two-launch and one-shot) with a rank dying
+    while every peer's tree kernel reads its send buffer -- the job aborts like the
+    reference (new_entry = -1, raben/errhandler.c:207-211)."""
+    o, r = _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, (1 << 18) + 3, seed=kill[0]), [kill],
+                  env={"FTAR_ONESHOT_MAX": form})
+    assert o.aborted
+
+
+@pytest.mark.parametrize("algo,p,kill,env", [("raben", 9, (6, 1, 1, 3), RELAY_ALL), ("raben", 9, (4, 2, 1, 3), RELAY_ALL),
+                                             ("rd", 8, (2, 1, 1, 3), RELAY_ALL), ("rd", 8, (5, 1, 2, 3), None),
+                                             ("rd", 6, (1, 1, 1, 3), None), ("raben", 9, (6, 1, 1, 3),
+                                                                             {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"})])
+def test_during_kill_transports(oracle, algo, p, kill, env):
+    """Mid-exchange deaths under the 2-hop relay (the victim is also a relay of other
+    receivers' stripes), the copy-engine transport, and recursive doubling (shrink branch
+    at p = 8, spare branch at p = 6)."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    _check(fn, algo, oracle.random_inputs(p, (1 << 20) + 7, seed=p * 10 + kill[0]), [kill], env=env)
+
+
+# ---- BASELINE configs at full size ---------------------------------------------------
+
+@pytest.mark.timeout(900)
+def test_full_size_c3_rd_p8(oracle):
+    """configs[2]: recursive doubling, 256 MiB float32 SUM, 8 ranks."""
+    _check(oracle.recursive_doubling, "rd", oracle.random_inputs(8, FULL, seed=703), timeout=600)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("shape", ["mesh", "reference"])
+def test_full_size_c4_raben_p8(oracle, shape):
+    """configs[3]: Rabenseifner, 256 MiB float32 SUM, 8 ranks -- the default one-hop
+    mesh, and the reference's shape (step by step, pairwise, step-0 full exchange)."""
+    # one device-resident 256 MiB call per rank (no host-pipeline chunking)
+    env = dict(REFERENCE_SHAPE if shape == "reference" else {}, FTAR_HOST_PIPE="0")
+    o, r = _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, FULL, seed=704), env=env, timeout=600)
+    mesh_steps = {st[0][9] for st in r.status.values()}
+    assert mesh_steps == ({2} if shape == "mesh" else {0}), r.status
+
+
+@pytest.mark.timeout(1200)
+def test_full_size_c5_p9_kill_mid_exchange(oracle):
+    """configs[4]: Rabenseifner, 256 MiB float32 SUM, 9 ranks (8 + idle spare), vrank 5
+    killed in reduce-scatter step 1 with its own 64 MiB pull kernel in flight and its
+    partner's pull reading its HBM: recovered, bit-exact to the oracle."""
+    kill = (6, 1, 1, 3)
+    o, r = _check(oracle.rabenseifner, "raben", oracle.random_inputs(9, FULL, seed=705), [kill], timeout=900,
+                  env={"FTAR_VERBOSE": "1"})
+    assert not o.aborted and o.recoveries == 1
+    in_flight, peers = _died_mid_exchange(r, 6)
+    assert peers >= 1
+    print(f"victim kernel in flight: {in_flight}, peers launched: {peers}")
+    assert "died mid-exchange at RS step 1" in r.stderr, r.stderr[-2000:]
+
+
+@pytest.mark.timeout(900)
+def test_full_size_mesh_p8_kill_mid_exchange_aborts(oracle):
+    """p = 8 at 256 MiB: a rank dies while the seven peers' tree kernels read its 256 MiB
+    send buffer over the mesh -- a clean abort, no hang, no device fault."""
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, FULL, seed=706), [(5, 1, 0, 3)], timeout=600)

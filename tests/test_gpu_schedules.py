@@ -240,7 +240,8 @@ def test_mesh_schedule(oracle, p, op, count):
     ins = oracle.random_inputs(p, count, seed=p * 7 + op, dtype=dt)
     if op >= 2:
         ins = H.with_specials(ins, p + op)
-    o, r = _check(oracle.rabenseifner, "raben", ins, op=op, env={"FTAR_ONESHOT_MAX": "0"})
+    # one device-resident call (the host pipeline would split >= 16 MiB into chunk calls)
+    o, r = _check(oracle.rabenseifner, "raben", ins, op=op, env={"FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0"})
     assert all(st[0][9] == 2 for st in r.status.values()), r.status
 
 

@@ -65,3 +65,51 @@ def test_multiple_kill_is_classified(hostsim, tmp_path, algo):
     r = rows[0]
     assert r["DEADLOCK"] == "False" and r["SEGFAULT"] == "False", (r, cp.stdout + cp.stderr)
     assert r["RIGHT RESULT"] == "True", r
+
+
+def test_launcher_never_a_kill_candidate(hostsim):
+    """run_mpi.sh passes the rank program through FTAR_PROG, so the reference killer's
+    rule (run/kill_procs.sh:12: R-state processes whose command line contains "main")
+    matches the rank processes but never `timeout` or the ftrun launcher, which sleeps in
+    sigtimedwait.  Sampled over a 2 s stretched run of a 4-rank job."""
+    import time
+    exe = os.path.join(ROOT, "tests", "hostsim", "_build", "src", "raben", "main")
+    env = dict(os.environ, FTAR_PROG=exe, FTAR_LOOP_SECONDS="2", FTAR_HOSTSIM_TAG=f"kc{os.getpid()}")
+    proc = subprocess.Popen(["timeout", "30", os.path.join(ROOT, "tests", "hostsim", "_build", "bin", "ftrun"),
+                             "-np", "4", "50000"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    seen_ranks, launchers, bad = set(), set(), set()
+    try:
+        t0 = time.time()
+        while proc.poll() is None and time.time() - t0 < 20:
+            rows = []
+            for line in subprocess.run(["ps", "-e", "-o", "pid=,ppid=,stat=,args="], capture_output=True,
+                                       text=True).stdout.splitlines():
+                f = line.split(None, 3)
+                if len(f) == 4:
+                    rows.append((int(f[0]), int(f[1]), f[2], f[3]))
+            tree = {proc.pid}
+            changed = True
+            while changed:
+                changed = False
+                for pid, ppid, _, _ in rows:
+                    if ppid in tree and pid not in tree:
+                        tree.add(pid)
+                        changed = True
+            for pid, ppid, st, args in rows:
+                if pid not in tree:
+                    continue
+                if ppid == proc.pid:
+                    launchers.add(pid)
+                if "main" in args and st.startswith("R"):  # the reference killer's candidates
+                    (bad if pid == proc.pid or ppid == proc.pid else seen_ranks).add(pid)
+            time.sleep(0.02)
+        out, err = proc.communicate(timeout=30)
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+        subprocess.run(f"rm -f /dev/shm/ftarhs-kc{os.getpid()}-*", shell=True)
+    assert proc.returncode == 0, err[-2000:]
+    assert launchers, "launcher never observed"
+    assert not bad, (bad, launchers)
+    assert seen_ranks, "no rank process was ever a candidate"
+    assert out.count("Hello from") == 4

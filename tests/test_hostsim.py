@@ -62,7 +62,7 @@ def test_single_kill_sweep(hostsim, oracle, algo, p):
     for v in range(p):
         for ph in phases:
             for st in range(4):
-                for pt in range(3):
+                for pt in range(4):
                     ks = [(v, ph, st, pt)]
                     if fn(ins, ks).status[v] != oracle.DEAD:
                         continue
@@ -78,7 +78,7 @@ def test_multi_kill_random(hostsim, oracle, seed):
     p = rng.choice([6, 7, 9, 11, 13, 17])
     nk = rng.choice([1, 2, 3])
     victims = rng.sample(range(p), nk)
-    kills = [(v, rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(4), rng.randrange(3)) for v in victims]
+    kills = [(v, rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(4), rng.randrange(4)) for v in victims]
     _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 511, seed=seed), kills)
 
 
@@ -220,7 +220,7 @@ def test_relay_single_kill_sweep(hostsim, oracle, algo, p):
     for v in range(p):
         for ph in phases:
             for st in range(3):
-                for pt in range(3):
+                for pt in range(4):
                     ks = [(v, ph, st, pt)]
                     if fn(ins, ks).status[v] != oracle.DEAD:
                         continue
@@ -235,7 +235,7 @@ def test_relay_multi_kill_random(hostsim, oracle, seed):
     algo = rng.choice(["raben", "rd"])
     p = rng.choice([6, 7, 9, 11])
     victims = rng.sample(range(p), rng.choice([1, 2]))
-    kills = [(v, rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(3), rng.randrange(3)) for v in victims]
+    kills = [(v, rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(3), rng.randrange(4)) for v in victims]
     _cmp(_fn(oracle, algo), algo, oracle.random_inputs(p, 2049, seed=seed), kills, env=RELAY_ALL)
 
 
@@ -258,11 +258,12 @@ def test_copy_engine_single_kill_sweep(hostsim, oracle, algo, p):
     for v in range(p):
         for ph in phases:
             for st in range(3):
-                ks = [(v, ph, st, 2)]
-                if fn(ins, ks).status[v] != oracle.DEAD:
-                    continue
-                _cmp(fn, algo, ins, ks, env=CE)
-                n += 1
+                for pt in (2, 3):  # BARRIER, DURING (copies in flight)
+                    ks = [(v, ph, st, pt)]
+                    if fn(ins, ks).status[v] != oracle.DEAD:
+                        continue
+                    _cmp(fn, algo, ins, ks, env=CE)
+                    n += 1
     assert n > 0
 
 
@@ -353,7 +354,7 @@ def test_mesh_single_kill_sweep(hostsim, oracle, p, form):
     for v in range(p):
         for ph in (0, 1, 2, 3):
             for st in range(3):
-                for pt in range(3):
+                for pt in range(4):
                     ks = [(v, ph, st, pt)]
                     if oracle.rabenseifner(ins, ks).status[v] != oracle.DEAD:
                         continue
@@ -466,7 +467,7 @@ def test_operand_order_specials_recovery(hostsim, oracle, algo, p, op):
     for v in range(p):
         for ph in range(4):
             for st in range(3):
-                for pt in range(3):
+                for pt in range(4):
                     o = fn(ins, [(v, ph, st, pt)], op=op)
                     if o.aborted or oracle.DEAD not in o.status:
                         continue
@@ -484,7 +485,7 @@ def test_raben_two_failures_random(hostsim, oracle, seed):
     import random
     rnd = random.Random(seed)
     p = 11
-    pts = [(v, ph, st, pt) for v in range(p) for ph in (1, 2) for st in range(3) for pt in range(3)]
+    pts = [(v, ph, st, pt) for v in range(p) for ph in (1, 2) for st in range(3) for pt in range(4)]
     ins = H.with_specials(oracle.random_inputs(p, 1031, seed=p + seed), p + seed)
     n = 0
     for ks in [((4, 1, 1, 2), (0, 1, 2, 1)), ((8, 1, 2, 0), (10, 1, 1, 0))] + [tuple(rnd.sample(pts, 2))
@@ -510,3 +511,47 @@ def test_two_barrier_victims_same_step(hostsim, oracle, algo, ks):
     ins = H.with_specials(oracle.random_inputs(p, 1031, seed=p + 78), p + 4)
     for op in (0, 2):
         _cmp(_fn(oracle, algo), algo, ins, list(ks), op=op)
+
+
+def test_staging_allocation_failure_aborts_job(hostsim, oracle):
+    """A rank whose pinned staging allocation fails (the _host entry points) ends the job
+    with MPI_Abort instead of returning alone while its peers wait in the collective;
+    nothing is left half-allocated for a later call to run into."""
+    ins = oracle.random_inputs(4, 1031, seed=41)
+    r = H.run_probe("raben", ins, iters=2, backend="hostsim", timeout=60,
+                    env_extra={"FTAR_HOSTSIM_FAIL_PLAIN": "1", "FTAR_HOSTSIM_FAIL_RANK": "2"})
+    assert r.aborted, r.stderr[-1000:]
+    assert "staging allocation" in r.stderr and r.returncode == 102, (r.returncode, r.stderr[-1000:])
+    assert not r.outputs
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+def test_torchrun_bootstrap(hostsim, oracle, tmp_path, algo):
+    """ftar_init's torchrun branch (RANK / WORLD_SIZE / MASTER_PORT, no ftrun): the
+    control block is named after the port and the elastic agent's pid, rank 0 creates
+    it -- the bootstrap bench.py uses at N > 1.  Two ranks, bit-exact to the oracle."""
+    import sys
+    import socket
+    p = 2
+    ins = oracle.random_inputs(p, 4099, seed=77)
+    for r_, x in enumerate(ins):
+        x.tofile(str(tmp_path / f"in_{r_}.bin"))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, FTAR_PROBE_DIR=str(tmp_path), FTAR_PROBE_ALGO=algo, FTAR_PROBE_DTYPE="1",
+               FTAR_PROBE_COUNT=str(ins[0].size), FTAR_HOSTSIM_TAG=f"tr{os.getpid()}", OMP_NUM_THREADS="1")
+    for k in ("FTAR_JOB", "FTAR_RANK", "FTAR_SIZE", "FTAR_LAUNCHER", "FTAR_KILL"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={p}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "--no-python",
+           os.path.join(hostsim, "bin", "ftar_probe")]
+    cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+    subprocess.run(f"rm -f /dev/shm/ftarhs-tr{os.getpid()}-*", shell=True)
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    o = oracle.rabenseifner(ins) if algo == "raben" else oracle.recursive_doubling(ins)
+    for r_ in range(p):
+        got = np.fromfile(str(tmp_path / f"out_{r_}_0.bin"), dtype=np.float32)
+        assert np.array_equal(got.view(np.uint32), o.outputs[r_].view(np.uint32)), r_
+        st = open(tmp_path / f"status_{r_}_0.txt").read().split()
+        assert st[0] == "0" and st[2] == str(p), st
