@@ -40,7 +40,7 @@ class Stats(ctypes.Structure):
                 ("hbm_bytes", ctypes.c_double), ("kernels", ctypes.c_int), ("step0_link_bytes", ctypes.c_double),
                 ("bg_kernel_ms", ctypes.c_double), ("sync_wait_s", ctypes.c_double),
                 ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int), ("relayed_steps", ctypes.c_int),
-                ("mesh_steps", ctypes.c_int)]
+                ("mesh_steps", ctypes.c_int), ("export_retries", ctypes.c_int)]
 
 
 class Kill(ctypes.Structure):

@@ -661,6 +661,7 @@ void ftar_stats_end(ftar_comm *c)
     c->stats.hbm_bytes += k.hbm_bytes;
     c->stats.kernels += k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3] + k.launches[4];
     c->stats.comm_size_after = c->size;
+    c->stats.export_retries = fdev_export_retries(c->dev);
     ftar_inputs_done(c);
 }
 

@@ -65,6 +65,8 @@ void fdev_close(ftar_dev *d);
 int fdev_device(const ftar_dev *d);
 
 int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle /* FDEV_HANDLE_BYTES */);
+/* blocks fdev_alloc_shared had to re-allocate because their IPC export was refused */
+int fdev_export_retries(const ftar_dev *d);
 int fdev_free(ftar_dev *d, void *ptr);
 int fdev_import(ftar_dev *d, const void *handle, void **ptr);
 /* Export the device allocation holding [ptr, ptr + bytes): its IPC handle, a per-process

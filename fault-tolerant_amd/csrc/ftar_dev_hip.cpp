@@ -21,6 +21,18 @@ namespace {
 char g_err[512];
 int g_reduce_variant = 1; // LDS-DMA staged (equal or faster than 0 in every C2 run)
 
+// Non-temporal 16-byte stores in every streaming kernel (FTAR_NT_STORE=0 turns them
+// off): see ftar_kernels.hip, measured on rotating buffers in profiles/r02.
+unsigned nt_store()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("FTAR_NT_STORE");
+        v = e ? (atoi(e) != 0) : 1;
+    }
+    return (unsigned)v;
+}
+
 int set_err(hipError_t e, const char *what)
 {
     snprintf(g_err, sizeof(g_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
@@ -80,6 +92,7 @@ struct ftar_dev {
         unsigned char handle[FDEV_HANDLE_BYTES];
     } exp[4];
     unsigned long long exp_clock;
+    int export_retries;
 };
 
 extern "C" {
@@ -159,17 +172,20 @@ void fdev_close(ftar_dev *d)
 
 int fdev_device(const ftar_dev *d) { return d->device; }
 
-// After memory has been exported and freed, a new hipMalloc of the same size can come
-// back at an address whose IPC export the runtime refuses (hipIpcGetMemHandle: invalid
-// argument; seen when the workspace grows mid-job).  Such a block is kept allocated
-// while the next one is tried, so the retry lands elsewhere, then all are freed.
+// Round 1 saw one refused export (hipIpcGetMemHandle: invalid argument) when a sweep
+// re-allocated the workspace at every size.  tools/ipc_probe.hip (profiles/r02) found no
+// refusal in the library's growth pattern -- 10 rounds of 4 blocks x 2 ranks, imports
+// closed before the free, closed-import VA ranges checked for reuse -- and the workspace
+// now grows geometrically, so a job re-allocates O(log S) times.  A refusal is still
+// handled, bounded and visible: the refused block is held while ONE more is tried (so the
+// retry lands at another address), the event is printed and counted
+// (ftar_stats.export_retries; tests assert it stays 0).
 int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
 {
     HIPCHK(hipSetDevice(d->device));
-    void *held[8];
-    int nheld = 0;
+    void *held = nullptr;
     hipError_t e = hipSuccess;
-    for (;;) {
+    for (int attempt = 0; attempt < 2; attempt++) {
         void *p = nullptr;
         e = hipMalloc(&p, bytes);
         if (e != hipSuccess) break;
@@ -178,16 +194,21 @@ int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
         if (e == hipSuccess) {
             memcpy(handle, &h, FDEV_HANDLE_BYTES);
             *ptr = p;
-            for (int i = 0; i < nheld; i++) (void)hipFree(held[i]);
+            if (held) (void)hipFree(held);
             return 0;
         }
         (void)hipGetLastError();
-        held[nheld++] = p;
-        if (nheld == 8) break;
+        fprintf(stderr, "ftar: device %d: IPC export of a fresh %zu B block at %p refused (%s)%s\n", d->device, bytes,
+                p, hipGetErrorString(e), attempt ? "" : ": re-allocating");
+        d->export_retries++;
+        if (held) (void)hipFree(held);
+        held = p;
     }
-    for (int i = 0; i < nheld; i++) (void)hipFree(held[i]);
+    if (held) (void)hipFree(held);
     return set_err(e, "hipMalloc + hipIpcGetMemHandle");
 }
+
+int fdev_export_retries(const ftar_dev *d) { return d->export_retries; }
 
 int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr)
 {
@@ -330,6 +351,7 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
     if (grid == 0) return 0;
+    L.nt_store = nt_store();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
         e0 = get_event(d);
@@ -372,6 +394,7 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
         for (int j = 0; j < nsrc; j++) A.src[j] = (const char *)src[j] + off * es;
         A.out = (char *)out + off * es;
         A.n = n - off < piece ? n - off : piece;
+        A.nt_store = nt_store();
         unsigned grid = ftar::plan_tree(&A, nsrc, es, d->max_blocks + 1);
         if (grid == 0) {
             snprintf(g_err, sizeof(g_err), "fdev_tree: plan failed");
@@ -406,6 +429,7 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
         for (int j = 0; j < nsrc; j++) A.src[j] = src[t * nsrc + j];
         A.out = out[t];
         A.n = n[t];
+        A.nt_store = nt_store();
         int nremote = __builtin_popcount(remote_mask[t] & ((1u << nsrc) - 1));
         link += (double)n[t] * (double)es * nremote;
         hbm += (double)n[t] * (double)es * (nsrc - nremote + 1);
@@ -683,7 +707,7 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
         size_t nv = n * es / 16;
         size_t tiles = (nv + ftar::kTileVecs - 1) / ftar::kTileVecs;
         unsigned grid = tiles < cached_blocks ? (unsigned)tiles : cached_blocks;
-        hipError_t e = ftar::launch_reduce_lds(dtype, op, inout, in, nv, grid, s);
+        hipError_t e = ftar::launch_reduce_lds(dtype, op, inout, in, nv, grid, s, nt_store());
         if (e != hipSuccess) return set_err(e, "reduce_lds_kernel launch");
         return 0;
     }
@@ -692,6 +716,7 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(&seg, 1, es, cached_blocks, &L);
     if (grid == 0) return 0;
+    L.nt_store = nt_store();
     hipError_t e = ftar::launch_segments(dtype, op, L, grid, s);
     if (e != hipSuccess) return set_err(e, "segment_kernel launch");
     return 0;

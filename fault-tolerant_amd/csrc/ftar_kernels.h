@@ -11,8 +11,8 @@ enum { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
 enum { kCopy = 0, kReduce = 1 };
 
 constexpr int kMaxKSegs = 48; // 16 user segments x (head, body, tail); 2.3 KB of kernarg
-constexpr int kTileVecs = 512; // 16-byte vectors per workgroup tile (256 threads x 2)
-constexpr int kChunkTiles = 8; // tiles per chunk of the interleaved block mapping (64 KiB)
+constexpr int kTileVecs = 1024; // 16-byte vectors per workgroup tile (256 threads x 4)
+constexpr int kChunkTiles = 8; // tiles per chunk of the interleaved block mapping (128 KiB)
 constexpr int kMaxIleave = 16; // vector pieces that can share the interleaved prefix
 
 struct KSeg {
@@ -39,6 +39,7 @@ struct KSegList {
     int nil;
     unsigned il_blocks;
     unsigned char il[kMaxIleave];
+    unsigned nt_store; // 16-byte stores non-temporal (set by the caller after plan_segments)
 };
 
 // What one workgroup of segment_kernel processes: piece `seg`, starting at tile (vector
@@ -91,6 +92,7 @@ struct TreeArgs {
     size_t head;   // scalar elements before the 16-byte vector body (co-aligned sources)
     size_t nv;     // 16-byte vectors in the body (0 when the pointers are not co-aligned)
     unsigned nvb;  // workgroups of the vector body; the rest do the scalar elements
+    unsigned nt_store; // 16-byte stores non-temporal
 };
 // fills the alignment fields of A (src/out/n set) and returns the grid size
 unsigned plan_tree(TreeArgs *A, int p, size_t esize, unsigned max_blocks);
@@ -109,6 +111,6 @@ hipError_t launch_tree_batch(int dtype, int op, int p, const TreeBatch &B, unsig
 unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_blocks, KSegList *L);
 hipError_t launch_segments(int dtype, int op, const KSegList &L, unsigned grid, hipStream_t s);
 hipError_t launch_reduce_lds(int dtype, int op, void *inout, const void *in, size_t nvec, unsigned grid,
-                             hipStream_t s);
+                             hipStream_t s, unsigned nt_store);
 
 } // namespace ftar

@@ -4,10 +4,10 @@
 // the operands, no reuse, no MFMA.  What matters on MI355X:
 //   * 16-byte lanes (global_load_dwordx4 / global_store_dwordx4): 1 KiB per wave
 //     instruction, the widest coalesced access;
-//   * enough bytes in flight and short-lived blocks: one 8 KiB tile per operand per
-//     256-thread workgroup, two independent 16-byte non-temporal loads per lane and
-//     operand, one tile per block (65536 workgroups for the 256 MiB C2 reduce) -- the
-//     fastest mapping of the C2 sweep (tools/reduce_sweep.hip);
+//   * enough bytes in flight and short-lived blocks: one 16 KiB tile per operand per
+//     256-thread workgroup, four independent 16-byte non-temporal loads per lane and
+//     operand, non-temporal stores, one tile per block (32768 workgroups for the 256 MiB
+//     C2 reduce) -- the fastest mapping of the rotating-buffer sweep (tools/hbm_sweep.hip);
 //   * one launch handles up to FDEV_MAX_KSEGS independent segments (e.g. Raben's
 //     step 0: reduce half the window + copy the other half of the partner's vector),
 //     blocks are split between segments in proportion to their bytes and each wave
@@ -65,24 +65,40 @@ __device__ __forceinline__ uint4 apply16(uint4 a, uint4 b)
 // segment kernel
 // ---------------------------------------------------------------------------------
 constexpr int kBlock = 256;
-constexpr int kUnroll = 2;
+// 4 x 16 B per lane and operand (16 KiB per operand per workgroup): 6.49-6.50 TB/s on
+// rotating buffers with nt stores against 6.14-6.20 for 2 and 6.05-6.09 for 8
+// (tools/hbm_sweep.hip, profiles/r02/hbm_sweep_focused.txt)
+constexpr int kUnroll = 4;
 static_assert(kBlock * kUnroll == kTileVecs, "tile size");
 
-// Streaming operands are read once: non-temporal loads (global_load_dwordx4 ... nt) keep
-// them from displacing useful lines and measured 6.36 TB/s against 5.2-5.5 TB/s for
-// plain loads on the C2 reduce (tools/reduce_sweep.hip, profiles/).  Stores stay plain:
-// non-temporal stores were slower in every configuration of that sweep.
+// Streaming operands are read once and results are not re-read by this kernel:
+// non-temporal loads AND stores (global_load/store_dwordx4 ... nt).  Timed on rotating
+// buffers (tools/hbm_sweep.hip: every launch on one of 4 pairs, 2 GiB, so the 256 MiB
+// Infinity Cache holds nothing the next launch reads) the C2 reduce runs at 6.2 TB/s
+// with nt stores against 5.6 TB/s with plain ones.  (Round 1's sweep looped over ONE
+// pair: there plain stores left the result in the Infinity Cache for the next launch to
+// read, which made them look faster -- an artefact of the benchmark, profiles/r02.)
+// `nts` is uniform over the launch (FTAR_NT_STORE, default on).
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ldnt(const uint4 *p)
 {
     v4u v = __builtin_nontemporal_load((const v4u *)p);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ void st16(uint4 *p, uint4 v, unsigned nts)
+{
+    if (nts) {
+        v4u w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, (v4u *)p);
+    } else {
+        *p = v;
+    }
+}
 
 template <typename T, int OP>
-__device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk)
+__device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk, unsigned nts)
 {
-    // Block-contiguous tiles of kBlock * kUnroll vectors (8 KiB per operand per block):
+    // Block-contiguous tiles of kBlock * kUnroll vectors (16 KiB per operand per block):
     // each lane issues kUnroll independent 16-byte non-temporal loads per operand, wave
     // instructions stay 1 KiB coalesced, and the grid is sized so that one tile per block
     // covers the segment (the loop only runs when the host capped the grid).
@@ -106,16 +122,16 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk)
                 for (int u = 0; u < kUnroll; u++) a[u] = apply16<T, OP>(a[u], c[u]);
             }
 #pragma unroll
-            for (int u = 0; u < kUnroll; u++) O[i + u * kBlock] = a[u];
+            for (int u = 0; u < kUnroll; u++) st16(O + i + u * kBlock, a[u], nts);
             if (O2) {
 #pragma unroll
-                for (int u = 0; u < kUnroll; u++) O2[i + u * kBlock] = a[u];
+                for (int u = 0; u < kUnroll; u++) st16(O2 + i + u * kBlock, a[u], nts);
             }
         } else {
             for (size_t j = i; j < nv; j += kBlock) {
                 const uint4 v = (S.kind == kCopy) ? ldnt(X + j) : apply16<T, OP>(ldnt(X + j), ldnt(Y + j));
-                O[j] = v;
-                if (O2) O2[j] = v;
+                st16(O + j, v, nts);
+                if (O2) st16(O2 + j, v, nts);
             }
         }
     }
@@ -143,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void segment_kernel(KSegList L)
     const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     const BlockWork w = map_block(L, b);
     const KSeg &S = L.s[__builtin_amdgcn_readfirstlane(w.seg)];
-    if (S.vec) vec_body<T, OP>(S, w.first, w.stride);
+    if (S.vec) vec_body<T, OP>(S, w.first, w.stride, L.nt_store);
     else scalar_body<T, OP>(S, w.first, w.stride);
 }
 
@@ -154,9 +170,9 @@ __global__ __launch_bounds__(kBlock) void segment_kernel(KSegList L)
 // the only ordering needed is the wave's own vmcnt(0) -- no workgroup barrier.
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(uint4 *__restrict__ inout,
-                                                            const uint4 *__restrict__ in, size_t nv)
+                                                            const uint4 *__restrict__ in, size_t nv, unsigned nts)
 {
-    __shared__ uint4 stage[kUnroll * kBlock]; // 16 KiB per workgroup
+    __shared__ uint4 stage[kUnroll * kBlock]; // 16 KiB per workgroup (kUnroll = 4)
     const int wave = threadIdx.x >> 6;
     const size_t tile = (size_t)kUnroll * kBlock;
     for (size_t base = (size_t)blockIdx.x * tile; base < nv; base += (size_t)gridDim.x * tile) {
@@ -174,10 +190,10 @@ __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(uint4 *__restrict__ 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
             for (int u = 0; u < kUnroll; u++)
-                inout[base + (size_t)u * kBlock + threadIdx.x] =
-                    apply16<T, OP>(a[u], stage[u * kBlock + threadIdx.x]);
+                st16(inout + base + (size_t)u * kBlock + threadIdx.x, apply16<T, OP>(a[u], stage[u * kBlock + threadIdx.x]),
+                     nts);
         } else {
-            for (size_t i = base + threadIdx.x; i < nv; i += kBlock) inout[i] = apply16<T, OP>(inout[i], in[i]);
+            for (size_t i = base + threadIdx.x; i < nv; i += kBlock) st16(inout + i, apply16<T, OP>(inout[i], in[i]), nts);
         }
     }
 }
@@ -200,7 +216,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs &A, unsigned b, unsigne
         for (int w = 1; w < P; w <<= 1)
 #pragma unroll
             for (int j = 0; j < P; j += 2 * w) v[j] = apply16<T, OP>(v[j], v[j + w]);
-        ((uint4 *)((T *)A.out + A.head))[i] = v[0];
+        st16((uint4 *)((T *)A.out + A.head) + i, v[0], A.nt_store);
         return;
     }
     constexpr size_t E = 16 / sizeof(T);
@@ -369,28 +385,29 @@ hipError_t launch_segments(int dtype, int op, const KSegList &L, unsigned grid, 
 }
 
 template <typename T>
-static hipError_t launch_lds_t(int op, uint4 *inout, const uint4 *in, size_t nv, unsigned grid, hipStream_t s)
+static hipError_t launch_lds_t(int op, uint4 *inout, const uint4 *in, size_t nv, unsigned grid, hipStream_t s,
+                               unsigned nts)
 {
     switch (op) {
-    case kSum: hipLaunchKernelGGL((reduce_lds_kernel<T, kSum>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv); break;
-    case kProd: hipLaunchKernelGGL((reduce_lds_kernel<T, kProd>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv); break;
-    case kMax: hipLaunchKernelGGL((reduce_lds_kernel<T, kMax>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv); break;
-    case kMin: hipLaunchKernelGGL((reduce_lds_kernel<T, kMin>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv); break;
+    case kSum: hipLaunchKernelGGL((reduce_lds_kernel<T, kSum>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv, nts); break;
+    case kProd: hipLaunchKernelGGL((reduce_lds_kernel<T, kProd>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv, nts); break;
+    case kMax: hipLaunchKernelGGL((reduce_lds_kernel<T, kMax>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv, nts); break;
+    case kMin: hipLaunchKernelGGL((reduce_lds_kernel<T, kMin>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv, nts); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_reduce_lds(int dtype, int op, void *inout, const void *in, size_t nvec, unsigned grid,
-                             hipStream_t s)
+                             hipStream_t s, unsigned nts)
 {
     uint4 *io = (uint4 *)inout;
     const uint4 *i = (const uint4 *)in;
     switch (dtype) {
-    case kInt32: return launch_lds_t<int32_t>(op, io, i, nvec, grid, s);
-    case kFloat32: return launch_lds_t<float>(op, io, i, nvec, grid, s);
-    case kInt64: return launch_lds_t<int64_t>(op, io, i, nvec, grid, s);
-    case kFloat64: return launch_lds_t<double>(op, io, i, nvec, grid, s);
+    case kInt32: return launch_lds_t<int32_t>(op, io, i, nvec, grid, s, nts);
+    case kFloat32: return launch_lds_t<float>(op, io, i, nvec, grid, s, nts);
+    case kInt64: return launch_lds_t<int64_t>(op, io, i, nvec, grid, s, nts);
+    case kFloat64: return launch_lds_t<double>(op, io, i, nvec, grid, s, nts);
     default: return hipErrorInvalidValue;
     }
 }
@@ -400,6 +417,7 @@ hipError_t launch_reduce_lds(int dtype, int op, void *inout, const void *in, siz
 unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_blocks, KSegList *L)
 {
     L->nseg = 0;
+    L->nt_store = 0;
     size_t vec_bytes_total = 0;
     struct Piece { KSeg k; size_t bytes; } pieces[kMaxKSegs];
     int np = 0;

@@ -78,8 +78,8 @@ int main(int argc, char **argv)
     if (np < 1 || np > FTAR_MAX_RANKS || (!prog && ai >= argc)) usage();
     /* the ranks' argv: prog (FTAR_PROG or the first argument) + the remaining arguments */
     int rest = prog ? ai : ai + 1;
-    char **rargv = calloc((size_t)(argc - rest + 2), sizeof(char *));
-    if (!rargv) return 1;
+    char *rargv[argc - rest + 2];
+    rargv[argc - rest + 1] = NULL;
     rargv[0] = (char *)(prog ? prog : argv[ai]);
     for (int i = rest; i < argc; i++) rargv[1 + i - rest] = argv[i];
     g_n = np;

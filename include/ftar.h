@@ -201,6 +201,8 @@ typedef struct {
     int    syncs;            /* agree/barrier rounds */
     int    relayed_steps;    /* exchange steps striped over 2-hop relays */
     int    mesh_steps;       /* one-hop mesh exchanges (Raben reduce-scatter / allgather) */
+    int    export_retries;   /* workspace blocks the runtime refused to export (IPC) and that were
+                                re-allocated, cumulative since ftar_init (expected: 0) */
 } ftar_stats;
 
 int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);

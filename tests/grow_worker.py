@@ -35,8 +35,10 @@ def main():
                 break
         if msg != "ok":
             break
+    # the workspace was re-allocated and re-exported at every growth: every block's IPC
+    # export must have succeeded on the first try
     with open(os.path.join(os.environ["FTAR_PROBE_DIR"], f"grow_{rank}.txt"), "w") as f:
-        f.write(msg)
+        f.write(f"{msg} retries={comm.last_stats().export_retries}")
     comm.finalize()
     return 0
 

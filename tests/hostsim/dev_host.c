@@ -67,7 +67,7 @@ static int put_map(void *p, size_t n, const char *name, int own)
             g_map[i].n = n;
             g_map[i].own = own;
             g_map[i].id = own ? ++g_next_id : 0;
-            snprintf(g_map[i].name, sizeof(g_map[i].name), "%s", name);
+            snprintf(g_map[i].name, sizeof(g_map[i].name), "%.63s", name);
             return 0;
         }
     return -1;
@@ -322,3 +322,5 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
     memset(&d, 0, sizeof(d));
     return fdev_run(&d, dtype, op, &s, 1, 0);
 }
+
+int fdev_export_retries(const ftar_dev *d) { return 0; }

@@ -1,0 +1,168 @@
+// ipc_probe.hip -- why did hipIpcGetMemHandle refuse a fresh workspace block (round 1,
+// "invalid argument" when the workspace grew mid-job)?
+//
+// Two processes on GPU 0 (forked before any HIP call, a shared-memory barrier between
+// them).  Each phase prints one JSON line.
+//   importer_reuse: B imports A's block, closes the mapping, then hipMallocs blocks of
+//       the same and of larger sizes and exports each: does an export fail, and does the
+//       failing block overlap the VA range B's closed import occupied?
+//   growth: the library's workspace pattern -- both processes allocate 4 blocks, export,
+//       import the peer's 4, close them, free their own, grow x2, for 2 MiB .. 1 GiB --
+//       counting exports refused on the first try, with the overlap test.
+// Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/ipc_probe.hip -o tools/_build/ipc_probe
+#include <hip/hip_runtime.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#define NB 4
+#define MAXR 16
+
+struct Shm {
+    _Atomic int bar[2];
+    hipIpcMemHandle_t h[2][NB];
+    int fail;
+};
+
+static Shm *S;
+static int me;
+static int gen;
+
+static void barrier()
+{
+    gen++;
+    atomic_store(&S->bar[me], gen);
+    while (atomic_load(&S->bar[1 - me]) < gen) usleep(50);
+}
+
+struct Range {
+    uintptr_t b, e;
+};
+
+static bool overlaps(void *p, size_t n, const Range *r, int nr)
+{
+    uintptr_t b = (uintptr_t)p, e = b + n;
+    for (int i = 0; i < nr; i++)
+        if (b < r[i].e && r[i].b < e) return true;
+    return false;
+}
+
+static void importer_reuse()
+{
+    const size_t s = 64ull << 20;
+    void *x = nullptr;
+    if (me == 0) {
+        (void)hipMalloc(&x, s);
+        (void)hipIpcGetMemHandle(&S->h[0][0], x);
+    }
+    barrier();
+    if (me == 1) {
+        void *imp = nullptr;
+        hipError_t e = hipIpcOpenMemHandle(&imp, S->h[0][0], hipIpcMemLazyEnablePeerAccess);
+        Range r = {(uintptr_t)imp, (uintptr_t)imp + s};
+        (void)hipIpcCloseMemHandle(imp);
+        printf("{\"phase\": \"importer_reuse\", \"open\": %d, \"import_va\": \"%p\", \"allocs\": [", (int)e, imp);
+        const size_t sizes[] = {64ull << 20, 32ull << 20, 128ull << 20, 2ull << 20, 256ull << 20};
+        for (int i = 0; i < 5; i++) {
+            void *y = nullptr;
+            (void)hipMalloc(&y, sizes[i]);
+            hipIpcMemHandle_t h;
+            hipError_t ee = hipIpcGetMemHandle(&h, y);
+            if (ee != hipSuccess) (void)hipGetLastError();
+            printf("%s{\"MiB\": %zu, \"va\": \"%p\", \"overlaps_closed_import\": %s, \"export\": \"%s\"}", i ? ", " : "",
+                   sizes[i] >> 20, y, overlaps(y, sizes[i], &r, 1) ? "true" : "false", hipGetErrorString(ee));
+            (void)hipFree(y);
+        }
+        printf("]}\n");
+        fflush(stdout);
+    }
+    barrier();
+    if (me == 0) (void)hipFree(x);
+    barrier();
+}
+
+static void growth()
+{
+    Range closed[MAXR * NB];
+    int nclosed = 0, refused = 0, refused_overlap = 0, rounds = 0;
+    void *own[NB] = {};
+    size_t s = 2ull << 20;
+    char log[8192];
+    log[0] = 0;
+    int off = 0;
+    for (int r = 0; r < 10; r++, s *= 2, rounds++) {
+        for (int b = 0; b < NB; b++) {
+            (void)hipMalloc(&own[b], s);
+            hipError_t e = hipIpcGetMemHandle(&S->h[me][b], own[b]);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                refused++;
+                bool ov = overlaps(own[b], s, closed, nclosed);
+                refused_overlap += ov;
+                off += snprintf(log + off, sizeof(log) - off, "%s{\"round\": %d, \"MiB\": %zu, \"va\": \"%p\", "
+                                "\"overlaps_closed_import\": %s, \"err\": \"%s\"}", off ? ", " : "", r, s >> 20,
+                                own[b], ov ? "true" : "false", hipGetErrorString(e));
+                // keep it (like the library's retry) and try once more
+                void *again = nullptr;
+                (void)hipMalloc(&again, s);
+                e = hipIpcGetMemHandle(&S->h[me][b], again);
+                (void)hipFree(own[b]);
+                own[b] = again;
+                if (e != hipSuccess) {
+                    (void)hipGetLastError();
+                    S->fail = 1;
+                }
+            }
+        }
+        barrier();
+        void *imp[NB];
+        for (int b = 0; b < NB; b++) {
+            imp[b] = nullptr;
+            if (hipIpcOpenMemHandle(&imp[b], S->h[1 - me][b], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void)hipGetLastError();
+                S->fail = 1;
+            }
+        }
+        barrier();
+        for (int b = 0; b < NB; b++) {
+            if (imp[b] && nclosed < MAXR * NB) closed[nclosed++] = Range{(uintptr_t)imp[b], (uintptr_t)imp[b] + s};
+            if (imp[b]) (void)hipIpcCloseMemHandle(imp[b]);
+        }
+        barrier();
+        for (int b = 0; b < NB; b++) (void)hipFree(own[b]);
+    }
+    printf("{\"phase\": \"growth\", \"rank\": %d, \"rounds\": %d, \"refused_first_try\": %d, "
+           "\"refused_overlapping_closed_import\": %d, \"refusals\": [%s]}\n",
+           me, rounds, refused, refused_overlap, log);
+    fflush(stdout);
+}
+
+int main()
+{
+    S = (Shm *)mmap(nullptr, sizeof(Shm), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    memset(S, 0, sizeof(Shm));
+    pid_t kids[2];
+    for (int k = 0; k < 2; k++) {
+        kids[k] = fork();
+        if (kids[k] == 0) {
+            me = k;
+            if (hipSetDevice(0) != hipSuccess) _exit(3);
+            importer_reuse();
+            growth();
+            _exit(0);
+        }
+    }
+    int rc = 0;
+    for (int k = 0; k < 2; k++) {
+        int st = 0;
+        waitpid(kids[k], &st, 0);
+        if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) rc = 1;
+    }
+    printf("{\"phase\": \"done\", \"ok\": %s, \"fail\": %d}\n", rc ? "false" : "true", S->fail);
+    return rc;
+}
