@@ -3,6 +3,7 @@ analysis/check_compare.py -> data_compare CSVs (the reference's slurm/test_compa
 analysis/check_compare.py layout)."""
 import csv
 import importlib.util
+import json
 import os
 import subprocess
 
@@ -134,3 +135,29 @@ def test_analyze_clean_sampling(tmp_path):
     # deterministic (seed 42 before every class pair, as clean_data.py)
     a.clean(str(src), str(tmp_path / "out2.csv"), [5, 9])
     assert (tmp_path / "out.csv").read_text() == (tmp_path / "out2.csv").read_text()
+
+
+def test_analyze_figures(tmp_path):
+    """Every figure of the reference's analysis scripts is produced (matplotlib, Agg):
+    compare panels + ratio, the 0-vs-1-killed boxplot, the outcome pie, and bench.py's
+    size sweep (FT vs RCCL)."""
+    a = _analyze()
+    ft, orig = tmp_path / "rd.csv", tmp_path / "original_rd.csv"
+    ft.write_text("NP;SIZE;TIME;RESULT\n" + "".join(f"{n};{s};{s * 1e-6 * n};0\n" for n in (4, 8) for s in (1, 64, 4096)))
+    orig.write_text("NP;SIZE;TIME;RESULT\n" + "".join(f"{n};{s};{s * 5e-7 * n};0\n" for n in (4, 8) for s in (1, 64, 4096)))
+    a.plot_compare(a.compare_table(str(ft), str(orig), "RD"), "RD", str(tmp_path / "cmp.png"))
+    log = tmp_path / "log.csv"
+    log.write_text("N;DELAY;BUF SIZE;KILLED;TIME;DEADLOCK;SEGFAULT;ABORT;RIGHT RESULT\n" +
+                   "".join(f"{n};2;100;{k};{1 + k + i / 10};False;False;{'True' if k and i == 0 else 'False'};True\n"
+                           for n in (5, 9) for k in (0, 1) for i in range(5)))
+    a.plot_fault(a.fault_frame(str(log)), "Rabenseifner", str(tmp_path / "fault.png"))
+    cnt = a.outcome_counts(str(log))
+    assert cnt == {"recovered": 8, "abort_after_recovery": 2, "abort": 0, "wrong_result": 0, "deadlock": 0}
+    a.plot_outcomes(cnt, str(tmp_path / "pie.png"))
+    bj = tmp_path / "bench.json"
+    bj.write_text(json.dumps({"n_gpus": 8, "size_sweep_us": {
+        str(b): {"bytes": b, "raben_us": 50 + b / 1e4, "rd_us": 60 + b / 1e4, "rccl_us": 30 + b / 2e4,
+                 "raben_over_rccl": (50 + b / 1e4) / (30 + b / 2e4)} for b in (4, 1024, 1 << 20, 1 << 28)}}) + "\n")
+    a.plot_sweep(a.sweep_table(str(bj)), str(tmp_path / "sweep.png"))
+    for f in ("cmp.png", "fault.png", "pie.png", "sweep.png"):
+        assert (tmp_path / f).stat().st_size > 5000, f

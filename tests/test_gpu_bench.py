@@ -1,0 +1,68 @@
+"""bench.py's two paths as the driver runs them, on the one-GPU test box.
+
+N = 1: `python bench.py` -- one JSON line with the contract's keys, the roofline of the
+local-reduce kernel and the CPU baselines.
+N = 2: the path the driver's 8-GPU SCALE run takes (torchrun, one rank per GPU, ftar_init's
+torchrun bootstrap, every leg of the N > 1 line), rehearsed with both ranks on GPU 0
+(FTAR_DEVICE=0) and gloo for torch.distributed (RCCL refuses two ranks on one device),
+at 4 MiB per rank so it runs in seconds.  The configs[4] leg runs as 5 ranks (4 + one
+idle spare) because this box has one GPU.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _last_json(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, out[-2000:]
+    return json.loads(lines[-1])
+
+
+@pytest.mark.timeout(300)
+def test_bench_single_gpu_line():
+    cp = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "10", "--warmup", "2",
+                         "--no-cpu-baseline"], capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    d = _last_json(cp.stdout)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "dtype", "config", "roofline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 10 and d["roofline"]["bound"] == "hbm"
+    assert 0.3 < d["roofline"]["frac"] < 1.0, d["roofline"]
+    assert "rotating" in d["config"]["buffers"]
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_rank_scale_path():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, FTAR_DEVICE="0", FTAR_C5_RANKS="5")
+    for k in ("FTAR_JOB", "FTAR_RANK", "FTAR_SIZE", "FTAR_LAUNCHER", "FTAR_KILL"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--dist-backend", "gloo", "--no-variants", "--count", str(1 << 20), "--steps", "2", "--warmup", "1"]
+    cp = subprocess.run(cmd, capture_output=True, text=True, timeout=540, cwd=ROOT, env=env)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    d = _last_json(cp.stdout)
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["int32_rank_checksum_ok"] == {"raben": True, "rd": True}
+    assert d["max_abs_err_vs_rccl"] < 1e-5
+    assert d["config"]["schedule"] and d["config"]["transport"] == d["transport"]
+    assert d["reference_shape"]["ms_per_step"] > 0
+    cpu = d["cpu_baseline"]
+    assert cpu and cpu["value"] and cpu["cores"] == 2 and cpu["kind"] == "port", cpu
+    c5 = d["c5_single_kill"]
+    assert c5 and c5["recovered"], c5
+    assert c5["fault"]["calls"][1]["recoveries"] == 1 and c5["fault"]["survivors"] == 4
+    assert "mid-exchange" in c5["fault"].get("victim", ""), c5

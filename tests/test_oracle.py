@@ -181,3 +181,24 @@ def test_int32_wraparound(oracle):
 def test_zero_count(oracle):
     r = oracle.rabenseifner([np.zeros(0, np.int32)] * 4)
     assert r.ret == 14  # MPI_ERR_UNKNOWN from copy_buffer (raben/util.c:40-43)
+
+
+def test_reference_wrong_result_rows_are_harness_artefacts(oracle):
+    """The reference's campaign recorded RIGHT RESULT=False rows (data/data_fault, e.g.
+    log_single_Raben.csv `17;2.0;110124421;1;...;False`).  They are not recovery
+    failures: as many occur in runs where no rank died (KILLED=0: every rank printed its
+    Hello line, so no failure and no error handler ran and the schedule is deterministic)
+    -- 43 of 51 for RD, 8 of 21 for Raben -- at no lower a rate than with a kill, and
+    concentrated at N >= 24 where 4 N stdout lines of concurrently printing ranks pass
+    through one mpiexec output stream (check_fault.py:70-88 parses them).  For every
+    such N the schedule itself (the oracle, no fault) produces the reference's closed-form
+    checksum."""
+    rows = load_fault_outcomes()
+    for algo in ("rd", "raben"):
+        wrong = [r for r in rows if r["algo"] == algo and not r["right"]]
+        nokill = sum(r["count"] for r in wrong if r["killed"] == 0)
+        assert nokill >= 8 and nokill / sum(r["count"] for r in wrong) > 0.3
+        fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+        for n in sorted({r["N"] for r in wrong}):
+            o = fn(oracle.rank_inputs(n, 257))
+            assert all(oracle.checksum17(x) == oracle.expected_checksum(n, 257) for x in o.outputs), (algo, n)
