@@ -529,6 +529,11 @@ def multi(args):
     links = (world - 1) if meshed else (r - 1) if relayed else 1
     peak = links * XGMI_LINK_GBS
     achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernels' pulled bytes
+
+    def frac(x):
+        # a one-GPU rehearsal has no xGMI link in the path (every "peer" read is local
+        # HBM shared by all ranks): link-roofline fractions would mix yardsticks
+        return None if rehearsal else round(x, 4)
     schedule = {
         "mesh-oneshot": "Rabenseifner, one-shot mesh: every block in its owner's reduction tree in one launch "
                         "(power-of-two p, no spare)",
@@ -558,16 +563,22 @@ def multi(args):
                 "value": round(world * S / t_ref / 1e9, 2), "ms_per_step": round(t_ref * 1e3, 4),
                 "algbw_GBps": round(S / t_ref / 1e9, 2), "step0_kernel_ms": round(k_ref, 4),
                 "survey_ft_roofline_ms": round(t_survey * 1e3, 3),
-                "frac_of_survey_roofline": round(t_survey / t_ref, 4)},
+                "frac_of_survey_roofline": frac(t_survey / t_ref)},
             "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "link_GBps": XGMI_LINK_GBS,
                                        "links_per_step": links, "t_roof_ms": round(t_roof * 1e3, 3),
-                                       "frac": round(t_roof / t_rb, 4)},
+                                       "frac": frac(t_roof / t_rb)},
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
                          "peak": peak, "unit": "GB/s",
-                         "frac": round(achieved / peak, 4) if achieved else None,
-                         "traffic": None,
+                         "frac": frac(achieved / peak) if achieved else None,
+                         "rehearsal": rehearsal,
+                         # HBM bytes per launch from PMC exist for the one-GPU rehearsal only
+                         # (every peer on this device); on the node the peer reads hit the
+                         # peers' HBM and the counters of one device miss them
+                         "traffic": pmc_traffic(f"mesh_tree_p{world}_rehearsal") if rehearsal and meshed
+                         and not oneshot else None,
                          "traffic_note": "PMC counters of a peer-reading kernel are per device; not collected on "
-                                         "the 8-GPU node (profiles/ has the one-GPU rehearsal's)",
+                                         "the 8-GPU node (profiles/pmc_summary.json has the one-GPU rehearsal's: "
+                                         "tree and allgather kernels within 0.02 % of their algorithmic bytes)",
                          "kernel": ("Raben one-shot mesh: tree_batch_kernel, every block in its owner's tree"
                                     if oneshot
                                     else "Raben mesh reduce-scatter: tree_kernel over p-1 one-hop pulls" if meshed
