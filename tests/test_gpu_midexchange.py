@@ -144,3 +144,27 @@ def test_full_size_mesh_p8_kill_mid_exchange_aborts(oracle):
     """p = 8 at 256 MiB: a rank dies while the seven peers' tree kernels read its 256 MiB
     send buffer over the mesh -- a clean abort, no hang, no device fault."""
     _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, FULL, seed=706), [(5, 1, 0, 3)], timeout=600)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", [0, 1])
+def test_random_kill_points_gpu(oracle, seed):
+    """Random single kills (any victim, phase, step and point -- DURING weighted up) on
+    the GPU, p = 5 / 9 (one idle spare) and 6 / 8, both schedules, 1 Mi elements, MAX over
+    NaN / signed zeros so the recovery path shows in the bits: outcome class and every
+    survivor's result as the oracle's.  Twelve jobs per seed, each a real process
+    teardown, most with a peer's kernel reading the victim's HBM."""
+    import random
+    rng = random.Random(seed)
+    n = 0
+    while n < 12:
+        algo = rng.choice(["raben", "rd"])
+        p = rng.choice([5, 9] if algo == "raben" else [6, 8, 9])
+        kill = (rng.randrange(p), rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(3),
+                rng.choice([3, 3, 0, 1, 2]))
+        fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+        ins = H.with_specials(oracle.random_inputs(p, (1 << 20) + 3, seed=seed * 100 + n), p)
+        if fn(ins, [kill], op=2).status[kill[0]] != oracle.DEAD:
+            continue  # the schedule never reaches this point (e.g. a step it does not have)
+        _check(fn, algo, ins, [kill], op=2)
+        n += 1
