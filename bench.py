@@ -485,6 +485,9 @@ def multi(args):
             r, model = cpu_schedule("raben", world, args.count, 3)
             cpu = {"value": round(world * S / r["time_s"] / 1e9, 4), "unit": "GB/s", "cores": world, "kind": "port",
                    "cpu_model": model, "ms_per_call": round(r["time_s"] * 1e3, 2), "algbw_GBps": r["algbw_GBps"],
+                   # the reference's TIME is clock() of one rank: CPU seconds per rank process
+                   # (ranks spin, so it tracks wall time; it also covers init, fill, checksum)
+                   "cpu_s_per_rank_process": r["cpu_s_per_rank_whole_process"],
                    "sample": f"Rabenseifner (FT, the reference's step-by-step pairwise shape), {world} rank processes "
                              f"pinned one per core, 256 MiB float32 per rank through shared memory, median of 3 "
                              f"calls (driver Time: lines, max over ranks); value = {world} x 256 MiB / call time"}
