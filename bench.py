@@ -477,13 +477,34 @@ def multi(args):
     if nccl:
         zz = x.clone()
         t_nc, _ = timed(lambda: dist.all_reduce(zz))
+
+    def rank0_leg(tag, fn):
+        """fn() on rank 0 while the other ranks SLEEP: a torch.distributed barrier can
+        spin host threads, and the leg pins its own processes to cores.  Rank 0 signals
+        the end through a file; one barrier on each side."""
+        flag = os.path.join("/tmp", f"ftar-bench-{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}-{tag}")
+        dist.barrier()
+        res = None
+        if rank == 0:
+            try:
+                res = fn()
+            finally:
+                with open(flag, "w") as f:
+                    f.write("done")
+        else:
+            while not os.path.exists(flag):
+                time.sleep(0.05)
+        dist.barrier()
+        if rank == 0:
+            os.unlink(flag)
+        return res
+
     # The CPU baseline: the same schedule on this node's host cores, in this job, rank 0
-    # only (the others wait at the barrier), float32, the same 256 MiB per rank.
-    cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    # only (the others sleep), float32, the same 256 MiB per rank.
+    def cpu_leg():
         try:
             r, model = cpu_schedule("raben", world, args.count, 3)
-            cpu = {"value": round(world * S / r["time_s"] / 1e9, 4), "unit": "GB/s", "cores": world, "kind": "port",
+            return {"value": round(world * S / r["time_s"] / 1e9, 4), "unit": "GB/s", "cores": world, "kind": "port",
                    "cpu_model": model, "ms_per_call": round(r["time_s"] * 1e3, 2), "algbw_GBps": r["algbw_GBps"],
                    # the reference's TIME is clock() of one rank: CPU seconds per rank process
                    # (ranks spin, so it tracks wall time; it also covers init, fill, checksum)
@@ -492,18 +513,20 @@ def multi(args):
                              f"pinned one per core, 256 MiB float32 per rank through shared memory, median of 3 "
                              f"calls (driver Time: lines, max over ranks); value = {world} x 256 MiB / call time"}
         except Exception as e:
-            cpu = {"value": None, "unit": "GB/s", "cores": world, "kind": "port", "sample": f"failed: {str(e)[-300:]}"}
-    dist.barrier()
+            return {"value": None, "unit": "GB/s", "cores": world, "kind": "port", "sample": f"failed: {str(e)[-300:]}"}
+
+    cpu = None if args.no_cpu_baseline else rank0_leg("cpu", cpu_leg)
+
     # configs[4]: the single-kill leg, its own ftrun job (rank 0), after everything else
-    c5 = None
-    if rank == 0 and not args.no_c5:
+    def c5_run():
         # this job's GPUs (LOCAL_RANK = GPU on one node), or the one GPU of a rehearsal
         devices = [dev] if rehearsal else list(range(world))
         try:
-            c5 = c5_leg(world, devices, args.count, int(os.environ.get("FTAR_C5_RANKS", "9")))
+            return c5_leg(world, devices, args.count, int(os.environ.get("FTAR_C5_RANKS", "9")))
         except Exception as e:
-            c5 = {"error": str(e)[-500:]}
-    dist.barrier()
+            return {"error": str(e)[-500:]}
+
+    c5 = None if args.no_c5 else rank0_leg("c5", c5_run)
     L = world.bit_length() - 1
     r = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
     # Link bytes per rank per direction.  The reference's FT Raben moves
