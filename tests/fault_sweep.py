@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--jobs", type=int, default=6)
     a = ap.parse_args()
     rnd = random.Random(a.seed)
-    pts = [(v, ph, st, pt) for v in range(a.p) for ph in (1, 2) for st in range(3) for pt in range(3)]
+    pts = [(v, ph, st, pt) for v in range(a.p) for ph in (1, 2) for st in range(3) for pt in range(4)]
     cases = []
     for algo in ("raben", "rd"):
         for _ in range(a.draws):

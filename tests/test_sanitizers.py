@@ -66,8 +66,11 @@ def test_asan_transports(asan_build, oracle, algo, p, env):
 
 @pytest.mark.parametrize("algo,p,kill", [("raben", 9, (5, 1, 1, 2)), ("raben", 9, (4, 2, 1, 1)),
                                          ("raben", 11, (3, 1, 2, 0)), ("rd", 8, (3, 1, 1, 2)),
-                                         ("rd", 6, (1, 1, 1, 2)), ("raben", 8, (2, 1, 1, 2))])
+                                         ("rd", 6, (1, 1, 1, 2)), ("raben", 8, (2, 1, 1, 2)),
+                                         ("raben", 9, (5, 1, 1, 3)), ("raben", 11, (2, 1, 2, 3)),
+                                         ("rd", 8, (3, 1, 1, 3))])
 def test_asan_recovery(asan_build, oracle, algo, p, kill):
     """Error handlers (impersonation replay, state hand-off, regroup; RD spare and shrink
-    branches) and the abort path, relayed where the windows allow it."""
+    branches) and the abort path, relayed where the windows allow it.  Point 3 kills the
+    victim mid-exchange (pre-image restore on the partner, late correction)."""
     _run(oracle, algo, oracle.random_inputs(p, 2053, seed=p + 400), [kill], env={"FTAR_RELAY_MIN": "0"})
