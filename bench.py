@@ -423,9 +423,12 @@ def multi(args):
             if name == "mesh" and not pow2:
                 continue
             set_opts(vals)
-            tv, _ = timed(raben)
+            tv, kv = timed(raben)
+            lb = timed.link_bytes
             tv_rd, _ = timed(rd) if name in ("relay2hop", "direct", "copy_engine") else (None, None)
-            transports[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2)}
+            transports[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2),
+                                "step0_kernel_ms": round(kv, 4), "step0_link_bytes": lb,
+                                "step0_pull_GBps": round(lb / (kv * 1e-3) / 1e9, 2) if kv > 0 else None}
             if tv_rd:
                 transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
         set_opts([chosen_opts[o] for o in opts])
@@ -560,6 +563,17 @@ def multi(args):
         # a one-GPU rehearsal has no xGMI link in the path (every "peer" read is local
         # HBM shared by all ranks): link-roofline fractions would mix yardsticks
         return None if rehearsal else round(x, 4)
+    # Link calibration ("B_link = the calibrated single-link unidirectional
+    # GB/s with both directions loaded"): the direct transport's RS step 0 is one kernel
+    # per rank pulling the partner's half over ONE link while the partner pulls ours, so
+    # its pulled bytes / its duration is that figure, measured in this job.
+    link_cal = None
+    dcal = transports.get("direct", {})
+    if dcal.get("step0_pull_GBps"):
+        link_cal = {"single_link_GBps": dcal["step0_pull_GBps"], "spec_GBps": XGMI_LINK_GBS,
+                    "frac_of_spec": frac(dcal["step0_pull_GBps"] / XGMI_LINK_GBS),
+                    "kernel": "direct transport, Raben RS step 0: pull the partner's half + reduce, both directions "
+                              "loaded", "bytes": dcal["step0_link_bytes"], "kernel_ms": dcal["step0_kernel_ms"]}
     schedule = {
         "mesh-oneshot": "Rabenseifner, one-shot mesh: every block in its owner's reduction tree in one launch "
                         "(power-of-two p, no spare)",
@@ -592,7 +606,12 @@ def multi(args):
                 "frac_of_survey_roofline": frac(t_survey / t_ref)},
             "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "link_GBps": XGMI_LINK_GBS,
                                        "links_per_step": links, "t_roof_ms": round(t_roof * 1e3, 3),
-                                       "frac": frac(t_roof / t_rb)},
+                                       "frac": frac(t_roof / t_rb),
+                                       # the same roofline priced at the calibrated link rate
+                                       "frac_calibrated_link": frac(t_roof * XGMI_LINK_GBS
+                                                                    / link_cal["single_link_GBps"] / t_rb)
+                                       if link_cal else None},
+            "link_calibration": link_cal,
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
                          "peak": peak, "unit": "GB/s",
                          "frac": frac(achieved / peak) if achieved else None,
