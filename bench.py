@@ -220,55 +220,65 @@ def e2e_local(ftar, count, iters=5):
             "GBps": round(2 * S * iters / ts["total"] / 1e9, 2)}
 
 
-def c5_leg(world, devices, count, ranks):
+def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
     """configs[4] on this node: `ranks` = world GPUs' worth of ranks + one idle spare (rank
-    1 shares rank 0's GPU), Rabenseifner 256 MiB float32 SUM, three calls per job; the
-    fault job kills vrank 5 (original rank 6) in reduce-scatter step 1 of call 1, mid-
-    exchange (its own pull kernel in flight, its partner's pull reading its HBM).  The
-    recovery shrinks the comm; call 2 runs on the survivors.  Run by rank 0 as a separate
-    ftrun job of bin/ftbench: torchrun's agent would tear the job down on a SIGKILL."""
+    1 shares rank 0's GPU), Rabenseifner 256 MiB float32 SUM, `calls` calls per job; the
+    fault job kills vrank 5 (original rank 6) in reduce-scatter step 1 of call `kill_call`,
+    mid-exchange (its own pull kernel in flight, its partner's pull reading its HBM).  The
+    recovery shrinks the comm; the later calls run on the survivors.  Call 0 is the warm-up
+    (workspace allocation, IPC imports).  Run by rank 0 as a separate ftrun job of
+    bin/ftbench: torchrun's agent would tear the job down on a SIGKILL."""
     exe = os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftbench")
     ftrun = os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftrun")
     devmap = [devices[0], devices[0]] + [devices[(r - 1) % len(devices)] for r in range(2, ranks)]
     victim = 6 if ranks > 6 else ranks - 1
     env = {k: v for k, v in os.environ.items()
            if not k.startswith(("FTAR_", "RANK", "LOCAL_", "WORLD_", "GROUP_", "ROLE_", "TORCHELASTIC"))}
-    res = {"ranks": ranks, "devmap": devmap, "count": count, "calls": 3,
-           "kill": f"{victim}:1:1:3 in call 1 (original rank {victim} = vrank {victim - 1}, reduce-scatter step 1, "
-                   "mid-exchange)"}
+    res = {"ranks": ranks, "devmap": devmap, "count": count, "calls": calls,
+           "kill": f"{victim}:1:1:3 in call {kill_call} (original rank {victim} = vrank {victim - 1}, reduce-scatter "
+                   "step 1, mid-exchange)"}
     want_all = float(sum(range(ranks)))
-    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:1")):
+    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}")):
         e = dict(env)
         if kill:
             e["FTAR_KILL"] = kill
         t0 = time.time()
         cp = subprocess.run([ftrun, "-np", str(ranks), "--devmap", ",".join(map(str, devmap)), exe, "raben",
-                             str(count), "3"], env=e, capture_output=True, text=True, timeout=600)
+                             str(count), str(calls)], env=e, capture_output=True, text=True, timeout=600)
         lines = [json.loads(l) for l in cp.stdout.splitlines() if l.startswith("{")]
-        calls = []
-        for c in range(3):
+        per_call = []
+        for c in range(calls):
             per = [ln["calls"][c] for ln in lines]
-            want = want_all - (victim if (kill and c == 2) else 0)
-            calls.append({"ms_max_over_ranks": round(max(p["ms"] for p in per), 3) if per else None,
-                          "recoveries": max((p["recoveries"] for p in per), default=None),
-                          "comm_size_after": min((p["comm_size"] for p in per), default=None),
-                          "result_ok": bool(per) and all(p["rc"] == 0 and p["uniform"] and p["value"] == want
-                                                         for p in per)})
+            # the kill call still sums every input (the dead rank's block is recovered,
+            # the reference's corr path); later calls sum the survivors'
+            want = want_all - (victim if (kill and c > kill_call) else 0)
+            per_call.append({"ms_max_over_ranks": round(max(p["ms"] for p in per), 3) if per else None,
+                             "recoveries": max((p["recoveries"] for p in per), default=None),
+                             "comm_size_after": min((p["comm_size"] for p in per), default=None),
+                             "result_ok": bool(per) and all(p["rc"] == 0 and p["uniform"] and p["value"] == want
+                                                            for p in per)})
         res[name] = {"rc": cp.returncode, "survivors": len(lines), "job_wall_s": round(time.time() - t0, 2),
-                     "calls": calls}
+                     "calls": per_call}
         if cp.returncode != 0 or not lines:
             res[name]["stderr_tail"] = cp.stderr[-600:]
         mid = [l for l in cp.stderr.splitlines() if "dies mid-exchange" in l]
         if mid:
             res[name]["victim"] = mid[0].split("ftar: ")[-1]
     f, n = res.get("fault", {}), res.get("no_fault", {})
+
+    def med(cs):
+        v = sorted(c["ms_max_over_ranks"] for c in cs)
+        return v[len(v) // 2]
     try:
-        res["recovered"] = f["survivors"] == ranks - 1 and f["calls"][1]["recoveries"] == 1 and \
-            all(c["result_ok"] for c in f["calls"])
-        res["recovered_call_ms"] = f["calls"][1]["ms_max_over_ranks"]
-        res["no_fault_call_ms"] = n["calls"][1]["ms_max_over_ranks"]
+        fc = f["calls"]
+        res["recovered"] = f["survivors"] == ranks - 1 and fc[kill_call]["recoveries"] == 1 and \
+            all(c["result_ok"] for c in fc)
+        res["recovered_call_ms"] = fc[kill_call]["ms_max_over_ranks"]
+        res["no_fault_call_ms"] = med(n["calls"][1:])  # median after the warm-up call
         res["recovery_overhead_ms"] = round(res["recovered_call_ms"] - res["no_fault_call_ms"], 3)
-    except (KeyError, IndexError, TypeError):
+        res["pre_fault_call_ms"] = med(fc[1:kill_call])
+        res["survivors_call_ms"] = med(fc[kill_call + 1:])  # p - 1 ranks after the shrink
+    except (KeyError, IndexError, TypeError, ValueError):
         res["recovered"] = False
     res["reference_leonardo_s"] = dict(REF_C5_S, note="clock() s per run incl. the whole MPI job, 460.6 MiB int32")
     return res

@@ -64,5 +64,7 @@ def test_bench_two_rank_scale_path():
     assert cpu and cpu["value"] and cpu["cores"] == 2 and cpu["kind"] == "port", cpu
     c5 = d["c5_single_kill"]
     assert c5 and c5["recovered"], c5
-    assert c5["fault"]["calls"][1]["recoveries"] == 1 and c5["fault"]["survivors"] == 4
+    kc = int(c5["kill"].split(" in call ")[1].split()[0])
+    assert c5["fault"]["calls"][kc]["recoveries"] == 1 and c5["fault"]["survivors"] == 4
+    assert all(c["result_ok"] for c in c5["no_fault"]["calls"]) and c5["survivors_call_ms"] > 0
     assert "mid-exchange" in c5["fault"].get("victim", ""), c5
