@@ -578,14 +578,14 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             if (x->vrank != -1 && !skip) {
                 const ftar_pull *pl = P.pull[x->rank];
                 void *PIN = ftar_buf(c, pl[0].src, WS_IN);
-                fdev_seg s0 = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, pl[0].off),
-                               at(x, ftar_local(c, pl[0].x_buf), pl[0].off), at(x, PIN, pl[0].off), (size_t)pl[0].n,
-                               NULL};
-                fdev_seg s1 = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
-                               (size_t)pl[1].n, NULL};
-                ftar_run_pulls(c, x->dtype, x->op, &s0, 1, FDEV_TAG_STEP0, 0);
+                fdev_seg red = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, pl[0].off),
+                                at(x, ftar_local(c, pl[0].x_buf), pl[0].off), at(x, PIN, pl[0].off), (size_t)pl[0].n,
+                                NULL};
+                fdev_seg cpy = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
+                                (size_t)pl[1].n, NULL};
+                ftar_run_pulls(c, x->dtype, x->op, &red, 1, FDEV_TAG_STEP0, 0);
                 if (x->keep_recov) {
-                    ftar_run_pulls(c, x->dtype, x->op, &s1, 1, FDEV_TAG_BG, 1);
+                    ftar_run_pulls(c, x->dtype, x->op, &cpy, 1, FDEV_TAG_BG, 1);
                     x->bg_pending = 1;
                 }
             }
