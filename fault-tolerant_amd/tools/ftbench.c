@@ -54,9 +54,15 @@ int main(int argc, char **argv)
     ftar_comm_device(comm, &dev);
     CHECK_HIP(hipSetDevice(dev));
 
+    /* FTBENCH_PATTERN=1: x_r[i] = (7 i + 13 r) mod 4096 instead of r, so every element
+     * has its own exact sum (all partial sums are integers < 2^24) and a misplaced
+     * window or a 32-bit index wrap shows as a wrong element (the size tests beyond
+     * 2^31 elements); "uniform" then means "every element equals its exact sum". */
+    const char *pe = getenv("FTBENCH_PATTERN");
+    const int pattern = pe && atoi(pe) != 0;
     float *h = malloc(count * sizeof(float));
     if (!h) return 4;
-    for (size_t i = 0; i < count; i++) h[i] = (float)wrank;
+    for (size_t i = 0; i < count; i++) h[i] = pattern ? (float)((7 * i + 13 * (size_t)wrank) % 4096) : (float)wrank;
     float *s = NULL, *r = NULL;
     CHECK_HIP(hipMalloc((void **)&s, count * sizeof(float)));
     CHECK_HIP(hipMalloc((void **)&r, count * sizeof(float)));
@@ -77,11 +83,19 @@ int main(int argc, char **argv)
         CHECK_HIP(hipMemcpy(h, r, count * sizeof(float), hipMemcpyDeviceToHost));
         value[c] = h[0];
         uniform[c] = 1;
-        for (size_t i = 1; i < count; i++)
-            if (h[i] != h[0]) {
+        const int members = size_after[c]; /* the original ranks 0 .. members-1 (no fault) */
+        for (size_t i = 0; i < count; i++) {
+            float want = h[0];
+            if (pattern) {
+                size_t sum = 0;
+                for (int q = 0; q < members; q++) sum += (7 * i + 13 * (size_t)q) % 4096;
+                want = (float)sum;
+            }
+            if (h[i] != want) {
                 uniform[c] = 0;
                 break;
             }
+        }
     }
     printf("{\"rank\": %d, \"size\": %d, \"device\": %d, \"calls\": [", wrank, wsize, dev);
     for (int c = 0; c < calls; c++)

@@ -9,7 +9,8 @@ Sources (read as CSV text; no reference code is imported or run):
       random single-kill campaign (run/run_test.sh with kill=1).
 
 Outputs (committed):
-  ref_checksums.csv       algo;NP;SIZE;RESULT  (subset: SIZE <= 2^20, one row per combination)
+  ref_checksums.csv       algo;NP;SIZE;RESULT  (one row per combination, every recorded SIZE up to
+                          the campaign's maximum 2^27)
   ref_fault_outcomes.csv  algo;N;KILLED;ABORT;DEADLOCK;RIGHT;count
 """
 import collections
@@ -27,8 +28,7 @@ def main():
         with open(os.path.join(REF, "data_compare", f"{algo}.csv")) as f:
             for r in csv.DictReader(f, delimiter=";"):
                 np_, size, res = int(r["NP"]), int(r["SIZE"]), int(r["RESULT"])
-                if size <= 2**20:
-                    rows.setdefault((algo, np_, size), res)
+                rows.setdefault((algo, np_, size), res)
     with open(os.path.join(HERE, "ref_checksums.csv"), "w") as f:
         f.write("algo;NP;SIZE;RESULT\n")
         for (algo, np_, size), res in sorted(rows.items()):

@@ -89,6 +89,28 @@ def test_reduce_local_c2_full_size(ftar, variant):
     assert torch.equal(y.view(torch.int32), want.view(torch.int32))
 
 
+@pytest.mark.parametrize("variant,extra", [(0, 4099), (1, 4100)])
+def test_reduce_local_beyond_2g_elements(ftar, variant, extra):
+    """More than 2^31 elements (8 GiB per vector): 64-bit indexing in both kernels and
+    the capped, grid-stride launch; a ragged tail for the register kernel.  Checked
+    against torch's fp32 add (one IEEE add per element, so bit-identical)."""
+    import torch
+    n = (1 << 31) + extra
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.rand(n, device="cuda", generator=g)
+    y = torch.rand(n, device="cuda", generator=g)
+    want = y + x
+    ftar.set_reduce_variant(variant)
+    try:
+        ftar.reduce_local(x, y, op=0)
+        torch.cuda.synchronize()
+    finally:
+        ftar.set_reduce_variant(0)
+    assert torch.equal(y.view(torch.int32), want.view(torch.int32))
+    del x, y, want
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("dt", [0, 1, 2, 3])
 def test_reduce_local_lds_variant_bit_exact(ftar, oracle, dt):
     import torch

@@ -157,6 +157,46 @@ def test_driver_golden_checksums(algo, p):
         assert set(hello.values()) == {want}, (size, hello, want)
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [4, 8])
+def test_driver_golden_checksums_max_size(algo, p):
+    """The reference's largest recorded size: 2^27 int32 (512 MiB) per rank
+    (data/data_compare/{raben,rd}.csv, e.g. raben.csv:29 `4;134217728;...;805306368`),
+    host buffers through the drop-in drivers, every rank's checksum equal to the
+    reference's RESULT."""
+    size = 1 << 27
+    want = _golden_checksums()[(algo, p, size)]
+    cp, hello = H.run_driver(algo, p, size, backend="gpu", env_extra={"FTAR_DEVMAP": ALL_ON_GPU0}, timeout=600)
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    assert sorted(hello) == list(range(p)), cp.stdout[-1000:]
+    assert set(hello.values()) == {want}, (hello, want)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("algo,p", [("raben", 2), ("rd", 2), ("raben", 3)])
+def test_beyond_2g_elements(algo, p):
+    """2^31 + 7 float32 elements per rank (8 GiB vectors, ~50 GiB of HBM per rank with the
+    workspace): the C ABI takes size_t counts (the reference's int count stops at 2^31-1).
+    bin/ftbench's pattern inputs x_r[i] = (7 i + 13 r) mod 4096 give every element its own
+    exact sum, checked element by element on the host: window offsets and 64-bit indexing
+    through the one-shot mesh (p = 2), recursive doubling and the pre-step path (p = 3)."""
+    import json
+    import subprocess
+    n = (1 << 31) + 7
+    env = dict(os.environ, FTBENCH_PATTERN="1")
+    env.pop("FTAR_KILL", None)
+    cp = subprocess.run([os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ALL_ON_GPU0,
+                         os.path.join(H.PKG, "bin", "ftbench"), algo, str(n), "1"], env=env, capture_output=True,
+                        text=True, timeout=800)
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    lines = [json.loads(ln) for ln in cp.stdout.splitlines() if ln.startswith("{")]
+    assert sorted(ln["rank"] for ln in lines) == list(range(p)), cp.stdout[-1000:]
+    for ln in lines:
+        c = ln["calls"][0]
+        assert c["rc"] == 0 and c["comm_size"] == p and c["uniform"], ln
+
+
 RELAY_ALL = {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}  # the step-by-step schedule, relayed
 
 
