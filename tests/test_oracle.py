@@ -2,7 +2,8 @@
 
 Golden data (tests/golden/, extracted by make_golden.py from the reference's data/ CSVs):
   * ref_checksums.csv: the per-rank checksum sum_i(result[i] % 17) printed by the
-    reference drivers for int32 SUM with buffer[i] = rank, NP in {4..64}, SIZE <= 2^20.
+    reference drivers for int32 SUM with buffer[i] = rank, NP in {4..64}, every recorded SIZE
+    (1 .. 2^27).
   * ref_fault_outcomes.csv: outcomes of the reference's random single-kill campaign.
 """
 import csv
