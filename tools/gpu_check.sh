@@ -36,7 +36,7 @@ if has smoke; then
 fi
 if has pytest; then
   FTAR_HEARTBEAT=$OUT/heartbeat.txt timeout -k 10 ${PYTEST_TIMEOUT:-1500} python -u -m pytest tests -m gpu -v \
-      --timeout 900 --timeout-method thread -p no:cacheprovider -rf ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+      --timeout 900 --timeout-method thread -p no:cacheprovider -rf --durations=25 ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; tail -6 "$OUT/pytest_gpu.log"; stop_on_fault $rc pytest
 fi
 if has bench; then
