@@ -540,6 +540,22 @@ def multi(args):
             return {"error": str(e)[-500:]}
 
     c5 = None if args.no_c5 else rank0_leg("c5", c5_run)
+
+    # The fabric itself (tools/xgmi_probe.hip, one process driving the job's GPUs): one
+    # link one way and both ways (SURVEY.md 8d's B_link), pull vs push, copy engines, and
+    # the all-peers pattern of the mesh.  A one-GPU rehearsal runs it in loopback.
+    def xgmi_leg():
+        exe = os.path.join(ROOT, "tools", "_build", "xgmi_probe")
+        try:
+            cp = subprocess.run([exe, str(1 if rehearsal else world)], capture_output=True, text=True, timeout=240)
+            lines = [ln for ln in cp.stdout.splitlines() if ln.startswith("{")]
+            if lines:
+                return json.loads(lines[-1])
+            return {"error": (cp.stderr or cp.stdout)[-300:], "rc": cp.returncode}
+        except Exception as e:
+            return {"error": str(e)[-300:]}
+
+    xgmi = None if args.no_xgmi else rank0_leg("xgmi", xgmi_leg)
     L = world.bit_length() - 1
     r = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
     # Link bytes per rank per direction.  The reference's FT Raben moves
@@ -579,11 +595,17 @@ def multi(args):
     # its pulled bytes / its duration is that figure, measured in this job.
     link_cal = None
     dcal = transports.get("direct", {})
-    if dcal.get("step0_pull_GBps"):
-        link_cal = {"single_link_GBps": dcal["step0_pull_GBps"], "spec_GBps": XGMI_LINK_GBS,
-                    "frac_of_spec": frac(dcal["step0_pull_GBps"] / XGMI_LINK_GBS),
-                    "kernel": "direct transport, Raben RS step 0: pull the partner's half + reduce, both directions "
-                              "loaded", "bytes": dcal["step0_link_bytes"], "kernel_ms": dcal["step0_kernel_ms"]}
+    probe = (xgmi or {}).get("patterns", {}).get("pull1_bidir", {})
+    if dcal.get("step0_pull_GBps") or probe.get("GBps_per_link"):
+        # the probe's plain copy over one link, both ways, where it ran on the node;
+        # otherwise the direct transport's step-0 pull
+        b = probe.get("GBps_per_link") if probe.get("ok") and probe.get("GBps_per_link") else dcal.get("step0_pull_GBps")
+        link_cal = {"single_link_GBps": b, "spec_GBps": XGMI_LINK_GBS, "frac_of_spec": frac(b / XGMI_LINK_GBS),
+                    "source": "xgmi_probe pull1_bidir" if b == probe.get("GBps_per_link") else "direct step 0",
+                    "direct_step0": {"kernel": "direct transport, Raben RS step 0: pull the partner's half + reduce, "
+                                               "both directions loaded", "bytes": dcal.get("step0_link_bytes"),
+                                     "kernel_ms": dcal.get("step0_kernel_ms"),
+                                     "pull_GBps": dcal.get("step0_pull_GBps")}}
     schedule = {
         "mesh-oneshot": "Rabenseifner, one-shot mesh: every block in its owner's reduction tree in one launch "
                         "(power-of-two p, no spare)",
@@ -622,6 +644,7 @@ def multi(args):
                                                                     / link_cal["single_link_GBps"] / t_rb)
                                        if link_cal else None},
             "link_calibration": link_cal,
+            "xgmi_probe": xgmi,
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
                          "peak": peak, "unit": "GB/s",
                          "frac": frac(achieved / peak) if achieved else None,
@@ -669,6 +692,7 @@ def main():
     ap.add_argument("--variant", type=int, default=1, help="local-reduce kernel: 0 register, 1 LDS-DMA (default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="N>1: skip the configs[4] single-kill leg")
+    ap.add_argument("--no-xgmi", action="store_true", help="N>1: skip the xGMI fabric probe")
     ap.add_argument("--timing", choices=["region", "launch"], default="region",
                     help="N=1 kernel time: events around the timed region, or around every launch")
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the transport comparison and size sweep")

@@ -68,3 +68,5 @@ def test_bench_two_rank_scale_path():
     assert c5["fault"]["calls"][kc]["recoveries"] == 1 and c5["fault"]["survivors"] == 4
     assert all(c["result_ok"] for c in c5["no_fault"]["calls"]) and c5["survivors_call_ms"] > 0
     assert "mid-exchange" in c5["fault"].get("victim", ""), c5
+    xg = d["xgmi_probe"]  # one GPU: the probe's kernels in loopback, destinations checked
+    assert xg and xg["ok"] and "loopback_copy" in xg["patterns"], xg

@@ -18,6 +18,7 @@
 #   e2e        host-buffer Raben end to end, chunk pipeline on / off
 #   syncprobe  tools/sync_probe.hip: device round trip of one step
 #   cpubase    tools/cpu_schedule_bench.py on this box's host cores
+#   xgmi       tools/xgmi_probe.hip: one link / all peers, pull / push / copy engines (loopback on one GPU)
 set -u
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
@@ -116,5 +117,9 @@ fi
 if has cpubase; then
   timeout -k 10 900 python tools/cpu_schedule_bench.py --out "$OUT/cpu_schedule_bench.json" > "$OUT/cpubase.log" 2>&1
   rc=$?; tail -c 600 "$OUT/cpu_schedule_bench.json"; stop_on_fault $rc cpubase
+fi
+if has xgmi; then
+  timeout -k 10 240 tools/_build/xgmi_probe > "$OUT/xgmi_probe.json" 2>&1
+  rc=$?; cat "$OUT/xgmi_probe.json"; stop_on_fault $rc xgmi
 fi
 echo ALLDONE
