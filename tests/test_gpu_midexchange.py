@@ -15,6 +15,8 @@ C5: p = 9 = 8 + one idle spare, a kill mid-exchange).  Every rank of these jobs 
 the one GPU of the test box, so the fabric is local HBM; the schedules, IPC mappings,
 control plane and recovery are the ones the 8-GPU node runs.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -148,8 +150,20 @@ def test_full_size_mesh_p8_kill_mid_exchange_aborts(oracle):
     _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, FULL, seed=706), [(5, 1, 0, 3)], timeout=600)
 
 
+def _seeds(var, default):
+    """Seeds of the random GPU kill tests; FTAR_GPU_KILL_SEEDS / FTAR_GPU_KILL2_SEEDS
+    ("2,3,4" or "2-11") widen a one-off campaign without editing the suite."""
+    v = os.environ.get(var)
+    if not v:
+        return default
+    if "-" in v:
+        a, b = v.split("-")
+        return list(range(int(a), int(b) + 1))
+    return [int(t) for t in v.split(",")]
+
+
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("seed", [0, 1])
+@pytest.mark.parametrize("seed", _seeds("FTAR_GPU_KILL_SEEDS", [0, 1]))
 def test_random_kill_points_gpu(oracle, seed):
     """Random single kills (any victim, phase, step and point -- DURING weighted up) on
     the GPU, p = 5 / 9 (one idle spare) and 6 / 8, both schedules, 1 Mi elements, MAX over
@@ -169,4 +183,31 @@ def test_random_kill_points_gpu(oracle, seed):
         if fn(ins, [kill], op=2).status[kill[0]] != oracle.DEAD:
             continue  # the schedule never reaches this point (e.g. a step it does not have)
         _check(fn, algo, ins, [kill], op=2)
+        n += 1
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", _seeds("FTAR_GPU_KILL2_SEEDS", [0]))
+def test_random_two_kills_gpu(oracle, seed):
+    """Two deaths in one call on the GPU (distinct victims, any phase / step / point,
+    mid-exchange weighted up): Raben p = 9 / 11 (one / three idle spares), RD p = 6 / 8,
+    MAX over NaN / signed zeros; outcome class and every survivor's bits as the oracle's
+    (the host-sim sweep tests/fault_sweep.py draws the same cases by the thousand)."""
+    import random
+    rng = random.Random(1000 + seed)
+    n = 0
+    while n < 6:
+        algo = rng.choice(["raben", "rd"])
+        p = rng.choice([9, 11] if algo == "raben" else [6, 8])
+        pts = [(v, ph, st, pt) for v in range(p) for ph in ((1, 2) if algo == "raben" else (1,))
+               for st in range(3) for pt in (3, 3, 0, 1, 2)]
+        kills = rng.sample(pts, 2)
+        if kills[0][0] == kills[1][0]:
+            continue
+        fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+        ins = H.with_specials(oracle.random_inputs(p, (1 << 18) + 3, seed=seed * 100 + n), p)
+        o = fn(ins, kills, op=2)
+        if sum(st == oracle.DEAD for st in o.status) < 2 and not o.aborted:
+            continue  # a point the schedule never reaches
+        _check(fn, algo, ins, kills, op=2)
         n += 1
