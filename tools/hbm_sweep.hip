@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_lds(v4f *__restrict__ io, const v4f *__
 
 // persistent grid-stride with a software pipeline: the next tile's loads are issued
 // before the current tile's stores
-template <int U, int NTL>
+template <int U, int NTL, int NTS = 0>
 __global__ __launch_bounds__(256) void k_pipe(v4f *__restrict__ io, const v4f *__restrict__ in, size_t nv)
 {
     const size_t tile = (size_t)U * 256;
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void k_pipe(v4f *__restrict__ io, const v4f *_
             for (int u = 0; u < U; u++) c[u] = ld<NTL>(in + base + u * 256);
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) io[cur + u * 256] = r[u];
+        for (int u = 0; u < U; u++) st<NTS>(io + cur + u * 256, r[u]);
         if (tn >= ntiles) break;
         t = tn;
     }
@@ -124,15 +124,15 @@ __global__ __launch_bounds__(256) void k_read(const v4f *__restrict__ in, v4f *_
     for (int u = 0; u < U; u++) s += ldnt(in + base + u * 256);
     if (s.x == 12345.f) sink[threadIdx.x] = s; // never true on the fill data
 }
-template <int U>
+template <int U, int NTS = 0>
 __global__ __launch_bounds__(256) void k_write(v4f *__restrict__ out, size_t nv)
 {
     const size_t base = (size_t)blockIdx.x * U * 256 + threadIdx.x;
     const v4f v = {1.f, 2.f, 3.f, (float)threadIdx.x};
 #pragma unroll
-    for (int u = 0; u < U; u++) out[base + u * 256] = v;
+    for (int u = 0; u < U; u++) st<NTS>(out + base + u * 256, v);
 }
-template <int U>
+template <int U, int NTS = 0>
 __global__ __launch_bounds__(256) void k_copy(v4f *__restrict__ out, const v4f *__restrict__ in, size_t nv)
 {
     const size_t base = (size_t)blockIdx.x * U * 256 + threadIdx.x;
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_copy(v4f *__restrict__ out, const v4f *
 #pragma unroll
     for (int u = 0; u < U; u++) a[u] = ldnt(in + base + u * 256);
 #pragma unroll
-    for (int u = 0; u < U; u++) out[base + u * 256] = a[u];
+    for (int u = 0; u < U; u++) st<NTS>(out + base + u * 256, a[u]);
 }
 
 __global__ void k_fill(v4f *p, size_t nv, float s)
@@ -211,6 +211,24 @@ int main(int argc, char **argv)
 #define LDSS(U, X, AUX, NS)                                                                                 \
     snprintf(nm, sizeof(nm), "lds U%d xcd%d aux%d nts%d", U, X, AUX, NS);                                  \
     run(nm, B3, true, [&](int r) { k_lds<U, X, AUX, NS><<<(unsigned)(nv / (U * 256)), 256>>>(io[r], in[r], nv); });
+    if (argc > 3 && argv[3][0] == 'g') { // nt-store calibration and persistent / pipelined grids
+        for (int rep = 0; rep < 2; rep++) {
+            run("read-only U4 (1 stream)", B1, false, [&](int r) { k_read<4><<<(unsigned)(nv / 1024), 256>>>(in[r], sink, nv); });
+            run("write-only U4 (1 stream)", B1, false, [&](int r) { k_write<4><<<(unsigned)(nv / 1024), 256>>>(io[r], nv); });
+            run("write-only U4 nt (1 stream)", B1, false, [&](int r) { k_write<4, 1><<<(unsigned)(nv / 1024), 256>>>(io[r], nv); });
+            run("copy U4 nt-store (2 streams)", B2, false, [&](int r) { k_copy<4, 1><<<(unsigned)(nv / 1024), 256>>>(io[r], in[r], nv); });
+            TILE(4, 256, 0, 1, 1)
+            LDSS(4, 0, 2, 1)
+            for (int G : {1024, 2048, 4096, 8192, 16384}) {
+                snprintf(nm, sizeof(nm), "pipe U4 ntl1 nts1 grid%d", G);
+                run(nm, B3, true, [&](int r) { k_pipe<4, 1, 1><<<G, 256>>>(io[r], in[r], nv); });
+                snprintf(nm, sizeof(nm), "pipe U2 ntl1 nts1 grid%d", G);
+                run(nm, B3, true, [&](int r) { k_pipe<2, 1, 1><<<G, 256>>>(io[r], in[r], nv); });
+            }
+        }
+        printf("BEST %s %.1f us %.1f GB/s\n", best, best_us, B3 / (best_us * 1e-6) / 1e9);
+        return 0;
+    }
     if (argc > 3 && argv[3][0] == 'f') { // focused: nt stores, three repetitions each
         for (int rep = 0; rep < 3; rep++) {
             TILE(2, 256, 0, 1, 1)
@@ -225,7 +243,7 @@ int main(int argc, char **argv)
             LDSS(4, 0, 0, 1)
             LDSS(4, 0, 2, 1)
             LDSS(2, 0, 0, 0)
-            run("copy U2 nt-store (2 streams)", B2, false, [&](int r) { k_copy<2><<<(unsigned)(nv / 512), 256>>>(io[r], in[r], nv); });
+            run("copy U2 nt-store (2 streams)", B2, false, [&](int r) { k_copy<2, 1><<<(unsigned)(nv / 512), 256>>>(io[r], in[r], nv); });
         }
         printf("BEST %s %.1f us %.1f GB/s\n", best, best_us, B3 / (best_us * 1e-6) / 1e9);
         return 0;
