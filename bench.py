@@ -322,15 +322,23 @@ def multi(args):
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        step0 = 0.0
+        step0 = kern = syncw = drain = 0.0
         for _ in range(steps):
             fn()
-            step0 += comm.last_stats().step0_kernel_ms
+            st = comm.last_stats()
+            step0 += st.step0_kernel_ms
+            kern += st.kernel_ms
+            syncw += st.sync_wait_s
+            drain += st.drain_s
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         dist.barrier()
-        t, k = max_over_ranks([t1 - t0, step0])
+        t, k, kall, sw, dr = max_over_ranks([t1 - t0, step0, kern, syncw, drain])
         timed.link_bytes = comm.last_stats().step0_link_bytes
+        # where a call's time goes (max over ranks of each part, per call)
+        timed.breakdown = {"call_ms": round(t / steps * 1e3, 4), "kernels_ms": round(kall / steps, 4),
+                           "dominant_kernel_ms": round(k / steps, 4), "agree_barrier_wait_ms": round(sw / steps * 1e3, 4),
+                           "stream_drain_wait_ms": round(dr / steps * 1e3, 4)}
         return t / steps, k / steps
 
     def timed_split(fn):
@@ -340,6 +348,7 @@ def multi(args):
         t, _ = timed(fn)
         comm.set_profiling(True)
         _, k = timed(fn, max(3, args.steps // 4), 1)
+        timed_split.breakdown = dict(timed.breakdown, profiled=True)
         return t, k
 
     def raben():
@@ -387,6 +396,7 @@ def multi(args):
 
     t_rb, k_rb = timed_split(raben)
     step0_bytes = timed.link_bytes
+    breakdown = timed_split.breakdown
     relayed = comm.last_stats().relayed_steps > 0
     meshed = comm.last_stats().mesh_steps > 0
     oneshot = comm.last_stats().mesh_steps == 1  # the mesh's one-launch form (p = 2, small vectors)
@@ -638,6 +648,9 @@ def multi(args):
                        "count": args.count, "parallelism": f"{world} ranks"},
             "algbw_GBps": round(S / t_rb / 1e9, 2),
             "transport": transport,
+            # the headline call of the profiled pass split into device time (all kernels /
+            # the dominant one) and the host's waits (agree + barrier rounds, stream drains)
+            "call_breakdown": breakdown,
             "reference_shape": {
                 "schedule": "Rabenseifner step by step, pairwise pulls (one xGMI link per step), step-0 full-vector "
                             "exchange kept (raben/rabenseifner.c:206-211)",
