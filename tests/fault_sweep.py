@@ -8,7 +8,7 @@ recovery that takes a different path than the oracle shows up even when the valu
 This sweep found the new-entry state hand-off and the BARRIER co-victim wait (DESIGN.md
 §3, "Second failure after a promotion").
 
-usage: python tests/fault_sweep.py [--p 11] [--kills 2] [--draws 400] [--seed 3] [--jobs 6]
+usage: python tests/fault_sweep.py [--p 11] [--kills 2] [--draws 400] [--seed 3] [--jobs 6] [--aborts]
 """
 import argparse
 import os
@@ -25,16 +25,20 @@ import harness as H  # noqa: E402
 import oracle as O  # noqa: E402
 
 
-def run_one(algo, p, op, kills, count):
+def run_one(algo, p, op, kills, count, aborts=False):
     ins = H.with_specials(O.random_inputs(p, count, seed=p + 78), p + 4)
     fn = O.rabenseifner if algo == "raben" else O.recursive_doubling
     o = fn(ins, list(kills), op=op)
-    if o.aborted or sum(s == O.DEAD for s in o.status) < len(kills):
+    if o.aborted and not aborts:
+        return None
+    if not o.aborted and sum(s == O.DEAD for s in o.status) < len(kills):
         return None
     try:
         r = H.run_probe(algo, ins, list(kills), op=op, backend="hostsim", timeout=30)
     except Exception:
         return "hang"
+    if o.aborted:  # the product must abort too (MPI_Abort line, no survivor output)
+        return "ok" if r.aborted and not r.outputs else "did not abort"
     if r.aborted:
         return "aborted"
     bad = [w for w in range(p) if o.status[w] == 0 and
@@ -50,6 +54,7 @@ def main():
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--count", type=int, default=1031)
     ap.add_argument("--jobs", type=int, default=6)
+    ap.add_argument("--aborts", action="store_true", help="also run the draws the oracle aborts (must abort)")
     a = ap.parse_args()
     rnd = random.Random(a.seed)
     pts = [(v, ph, st, pt) for v in range(a.p) for ph in (1, 2) for st in range(3) for pt in range(4)]
@@ -60,10 +65,11 @@ def main():
             if len({k[0] for k in ks}) == a.kills:
                 cases.append((algo, a.p, rnd.choice([0, 2, 3]), ks, a.count))
     with ThreadPoolExecutor(a.jobs) as ex:
-        res = list(ex.map(lambda c: run_one(*c), cases))
+        res = list(ex.map(lambda c: run_one(*c, aborts=a.aborts), cases))
     ran = [(c, r) for c, r in zip(cases, res) if r is not None]
     bad = [(c, r) for c, r in ran if r != "ok"]
-    print(f"{len(cases)} drawn, {len(ran)} recovering with {a.kills} deaths, {len(bad)} differ from the oracle")
+    what = "recovering or aborting" if a.aborts else "recovering"
+    print(f"{len(cases)} drawn, {len(ran)} {what} with {a.kills} deaths, {len(bad)} differ from the oracle")
     for c, r in bad[:20]:
         print("  ", c[0], "op", c[2], "kills", c[3], "->", r)
     sys.exit(1 if bad else 0)
