@@ -224,21 +224,26 @@ def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
     """configs[4] on this node: `ranks` = world GPUs' worth of ranks + one idle spare (rank
     1 shares rank 0's GPU), Rabenseifner 256 MiB float32 SUM, `calls` calls per job; the
     fault job kills vrank 5 (original rank 6) in reduce-scatter step 1 of call `kill_call`,
-    mid-exchange (its own pull kernel in flight, its partner's pull reading its HBM).  The
-    recovery shrinks the comm; the later calls run on the survivors.  Call 0 is the warm-up
-    (workspace allocation, IPC imports).  Run by rank 0 as a separate ftrun job of
-    bin/ftbench: torchrun's agent would tear the job down on a SIGKILL."""
+    mid-exchange (its own pull kernel in flight, its partner's pull reading its HBM), a
+    second one in allgather step 1 ("also AG step 1"; the last AG step when
+    there are only two).  The recovery shrinks the comm; the later calls run on the
+    survivors.  Call 0 is the warm-up (workspace allocation, IPC imports).  Run by rank 0
+    as separate ftrun jobs of bin/ftbench: torchrun's agent would tear the job down on a
+    SIGKILL."""
     exe = os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftbench")
     ftrun = os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftrun")
     devmap = [devices[0], devices[0]] + [devices[(r - 1) % len(devices)] for r in range(2, ranks)]
     victim = 6 if ranks > 6 else ranks - 1
+    ag_step = 1 if ranks >= 8 else 0  # a middle allgather step where there is one (L >= 3)
     env = {k: v for k, v in os.environ.items()
            if not k.startswith(("FTAR_", "RANK", "LOCAL_", "WORLD_", "GROUP_", "ROLE_", "TORCHELASTIC"))}
     res = {"ranks": ranks, "devmap": devmap, "count": count, "calls": calls,
            "kill": f"{victim}:1:1:3 in call {kill_call} (original rank {victim} = vrank {victim - 1}, reduce-scatter "
-                   "step 1, mid-exchange)"}
+                   "step 1, mid-exchange)",
+           "kill_ag": f"{victim}:2:{ag_step}:3 in call {kill_call} (allgather step {ag_step}, mid-exchange)"}
     want_all = float(sum(range(ranks)))
-    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}")):
+    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}"),
+                       ("fault_ag", f"{victim}:2:{ag_step}:3:{kill_call}")):
         e = dict(env)
         if kill:
             e["FTAR_KILL"] = kill
@@ -269,11 +274,16 @@ def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
     def med(cs):
         v = sorted(c["ms_max_over_ranks"] for c in cs)
         return v[len(v) // 2]
+    def recovered(job):
+        fc = job["calls"]
+        return job["survivors"] == ranks - 1 and fc[kill_call]["recoveries"] == 1 and all(c["result_ok"] for c in fc)
     try:
         fc = f["calls"]
-        res["recovered"] = f["survivors"] == ranks - 1 and fc[kill_call]["recoveries"] == 1 and \
-            all(c["result_ok"] for c in fc)
+        res["recovered_rs"] = recovered(f)
+        res["recovered_ag"] = recovered(res["fault_ag"])
+        res["recovered"] = res["recovered_rs"] and res["recovered_ag"]
         res["recovered_call_ms"] = fc[kill_call]["ms_max_over_ranks"]
+        res["recovered_ag_call_ms"] = res["fault_ag"]["calls"][kill_call]["ms_max_over_ranks"]
         res["no_fault_call_ms"] = med(n["calls"][1:])  # median after the warm-up call
         res["recovery_overhead_ms"] = round(res["recovered_call_ms"] - res["no_fault_call_ms"], 3)
         res["pre_fault_call_ms"] = med(fc[1:kill_call])

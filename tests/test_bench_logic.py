@@ -70,8 +70,10 @@ def test_c5_leg_summary(bench):
     assert res["pre_fault_call_ms"] == 2.0 and res["survivors_call_ms"] == 1.5
     assert res["recovery_overhead_ms"] == 1.5
     assert "dies mid-exchange" in f["victim"]
+    assert res["recovered_rs"] and res["recovered_ag"] and res["recovered_ag_call_ms"] == 3.5
+    assert res["kill_ag"].startswith("6:2:1:3 in call 2")
     runs = [json.loads(l) for l in open(tmp / "log.jsonl")]
-    assert [r["kill"] for r in runs] == [None, "6:1:1:3:2"]
+    assert [r["kill"] for r in runs] == [None, "6:1:1:3:2", "6:2:1:3:2"]
     assert runs[0]["argv"][-3:] == ["raben", "1024", "6"]
 
 
@@ -80,6 +82,7 @@ def test_c5_leg_rehearsal_layout(bench):
     m, _ = bench
     res = m.c5_leg(2, [0], 64, 5)
     assert res["devmap"] == [0, 0, 0, 0, 0] and res["kill"].startswith("4:1:1:3 in call 2")
+    assert res["kill_ag"].startswith("4:2:0:3 in call 2")  # two AG steps: the last one recovers
     assert res["recovered"] is True, res
 
 
