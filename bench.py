@@ -269,6 +269,7 @@ def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
         mid = [l for l in cp.stderr.splitlines() if "dies mid-exchange" in l]
         if mid:
             res[name]["victim"] = mid[0].split("ftar: ")[-1]
+    res["random_kill"] = c5_random_kill(ftrun, exe, ranks, devmap, count, env)
     f, n = res.get("fault", {}), res.get("no_fault", {})
 
     def med(cs):
@@ -292,6 +293,64 @@ def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
         res["recovered"] = False
     res["reference_leonardo_s"] = dict(REF_C5_S, note="clock() s per run incl. the whole MPI job, 460.6 MiB int32")
     return res
+
+
+def c5_random_kill(ftrun, exe, ranks, devmap, count, env, calls=3, loop_s=1.5, seed=0):
+    """The reference's random kill (run/kill_procs.sh: SIGKILL one rank process after a
+    random delay) on the configs[4] job: each call is stretched to `loop_s` seconds of
+    busy agree rounds (FTAR_LOOP_SECONDS, as run/run_mpi.sh does) so the kill lands inside
+    the schedule; the outcome is the reference's (recovered, or MPI_Abort where its
+    handler aborts), and every survivor's results must agree, call by call, on the exact
+    sum with or without the victim's input, never dropping it and taking it back."""
+    import random
+    import signal
+    rng = random.Random(seed)
+    victim = rng.randrange(ranks)
+    delay = rng.uniform(1.0, 1.0 + loop_s * calls)  # after the launch: ~1 s of process start-up
+    e = dict(env, FTAR_LOOP_SECONDS=str(loop_s))
+    out = {"victim": victim, "delay_s": round(delay, 3), "loop_seconds": loop_s, "calls": calls}
+    try:
+        import psutil
+        t0 = time.time()
+        pr = subprocess.Popen([ftrun, "-np", str(ranks), "--devmap", ",".join(map(str, devmap)), exe, "raben",
+                               str(count), str(calls)], env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        time.sleep(delay)
+        for k in psutil.Process(pr.pid).children():  # the rank processes ftrun started
+            try:
+                if k.environ().get("FTAR_RANK") == str(victim):
+                    os.kill(k.pid, signal.SIGKILL)
+                    out["killed"] = True
+            except (psutil.Error, OSError):
+                pass
+        so, se = pr.communicate(timeout=300)
+        out["job_wall_s"] = round(time.time() - t0, 2)
+    except Exception as ex:
+        out["error"] = str(ex)[-300:]
+        return out
+    lines = [json.loads(l) for l in so.splitlines() if l.startswith("{")]
+    full = float(sum(range(ranks)))
+    out["aborted"] = "MPI_ABORT" in se
+    out["survivors"] = len(lines)
+    consistent = bool(lines) or out["aborted"]
+    dropped = False
+    per = []
+    for c in range(calls):
+        vals = {ln["calls"][c]["value"] for ln in lines}
+        ok = len(vals) <= 1 and all(ln["calls"][c]["rc"] == 0 and ln["calls"][c]["uniform"] for ln in lines)
+        v = vals.pop() if len(vals) == 1 else None
+        if v is not None and v not in (full, full - victim):
+            ok = False
+        if dropped and v == full:
+            ok = False
+        dropped = dropped or v == full - victim
+        consistent = consistent and ok
+        per.append({"value": v, "recoveries": max((ln["calls"][c]["recoveries"] for ln in lines), default=None),
+                    "ms_max_over_ranks": round(max((ln["calls"][c]["ms"] for ln in lines), default=0.0), 3)})
+    out["per_call"] = per
+    out["outcome"] = "aborted" if out["aborted"] else "recovered" if len(lines) == ranks - 1 else \
+        "no fault hit" if len(lines) == ranks else "lost"
+    out["results_consistent"] = consistent
+    return out
 
 
 def multi(args):

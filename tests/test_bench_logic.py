@@ -52,6 +52,7 @@ def bench(tmp_path, monkeypatch):
     f.chmod(f.stat().st_mode | stat.S_IEXEC)
     (bindir / "ftbench").write_text("")
     monkeypatch.setattr(m, "ROOT", str(tmp_path))
+    monkeypatch.setattr(m, "c5_random_kill", lambda *a, **k: {"stub": True})
     monkeypatch.setenv("FAKE_LOG", str(tmp_path / "log.jsonl"))
     return m, tmp_path
 

@@ -68,5 +68,7 @@ def test_bench_two_rank_scale_path():
     assert c5["fault"]["calls"][kc]["recoveries"] == 1 and c5["fault"]["survivors"] == 4
     assert all(c["result_ok"] for c in c5["no_fault"]["calls"]) and c5["survivors_call_ms"] > 0
     assert "mid-exchange" in c5["fault"].get("victim", ""), c5
+    rk = c5["random_kill"]  # kill_procs.sh's random SIGKILL: any outcome, consistent results
+    assert rk.get("killed") and rk["outcome"] in ("recovered", "aborted") and rk["results_consistent"], rk
     xg = d["xgmi_probe"]  # one GPU: the probe's kernels in loopback, destinations checked
     assert xg and xg["ok"] and "loopback_copy" in xg["patterns"], xg
