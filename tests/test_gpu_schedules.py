@@ -410,3 +410,19 @@ def test_device_entry_refuses_pageable_host_memory(algo):
     assert r.returncode == 0, r.stderr[-2000:]
     for w in range(2):
         assert r.status[w][0][0] == 13 and r.status[w][1][0] == 13, r.status[w]
+
+
+@pytest.mark.parametrize("algo,p,env", [
+    ("raben", 4, {}), ("raben", 8, {"FTAR_ONESHOT_MAX": "0"}), ("raben", 2, {}),
+    ("raben", 9, {"FTAR_RELAY_MIN": "0"}), ("rd", 6, {"FTAR_RELAY_MIN": "0"}), ("rd", 8, {}),
+    ("raben", 9, {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"})])
+def test_capped_grids_plain_stores(oracle, algo, p, env):
+    """One workgroup per CU (FTAR_BLOCKS_PER_CU=1: 256-workgroup grids) so every kernel
+    strides over its pieces and the tree launches split, with plain instead of
+    non-temporal stores (FTAR_NT_STORE=0): the launch geometry and store flavour change,
+    the bits must not -- MAX over NaN / signed zeros pins every operand order."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    ins = H.with_specials(oracle.random_inputs(p, (1 << 20) + 37, seed=p * 13 + 5), p + 1)
+    _check(fn, algo, ins, op=2, env=dict(env, FTAR_BLOCKS_PER_CU="1", FTAR_NT_STORE="0"))
+    _check(fn, algo, oracle.random_inputs(p, (1 << 20) + 37, seed=p * 13 + 6),
+           env=dict(env, FTAR_BLOCKS_PER_CU="1"))
