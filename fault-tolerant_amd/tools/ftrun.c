@@ -196,6 +196,7 @@ int main(int argc, char **argv)
     int aborted = atomic_load(&job.shm->abort_flag);
     int code = aborted ? atomic_load(&job.shm->abort_code) : exit_code;
     shm_unlink(g_name);
-    if (!code && signalled) code = 0; /* tolerated failures: survivors finished cleanly */
+    if (!code && signalled == np) code = 128 + SIGKILL; /* every rank died: nobody finished */
+    /* otherwise some ranks died and the survivors finished cleanly: tolerated, 0 */
     return code;
 }

@@ -16,12 +16,18 @@ import numpy as np
 import pytest
 
 import harness as H
+import oracle as O
 
 
 def _cmp(oracle_fn, algo, inputs, kills=(), op=0, env=None):
     o = oracle_fn(inputs, kills, op=op)
     r = H.run_probe(algo, inputs, kills, op=op, backend="hostsim", timeout=120, env_extra=env)
     u = {4: np.uint32, 8: np.uint64}[inputs[0].dtype.itemsize]
+    if all(st == O.DEAD for st in o.status):
+        # every rank killed (e.g. p = 1): no survivor to detect it or to call MPI_Abort;
+        # the job is lost, as an mpiexec job of killed processes is
+        assert not r.outputs and r.returncode != 0, (kills, r.returncode, r.stderr[-1000:])
+        return o, r
     if o.aborted:
         assert r.aborted and not r.outputs, (kills, r.stderr[-1000:])
         return o, r
@@ -555,3 +561,33 @@ def test_torchrun_bootstrap(hostsim, oracle, tmp_path, algo):
         assert np.array_equal(got.view(np.uint32), o.outputs[r_].view(np.uint32)), r_
         st = open(tmp_path / f"status_{r_}_0.txt").read().split()
         assert st[0] == "0" and st[2] == str(p), st
+
+
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+TRANSPORTS = [{}, {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}, {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"},
+              {"FTAR_MESH": "0", "FTAR_RELAY": "0", "FTAR_OVERLAP": "0"}, {"FTAR_EXPORT": "0"},
+              {"FTAR_ONESHOT_MAX": "0"}, {"FTAR_REDUNDANCY": "1", "FTAR_MESH": "0"}]
+
+
+@settings(max_examples=int(os.environ.get("FTAR_PROPERTY_EXAMPLES", "120")), deadline=None,
+          suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(algo=st.sampled_from(["raben", "rd"]), p=st.integers(1, 13), count=st.integers(1, 3000),
+       dtype=st.sampled_from([np.float32, np.int32, np.int64, np.float64]), op=st.integers(0, 3),
+       transport=st.integers(0, len(TRANSPORTS) - 1), kill=st.none() | st.tuples(
+           st.integers(0, 12), st.integers(0, 3), st.integers(0, 3), st.integers(0, 3)),
+       seed=st.integers(0, 10 ** 6))
+def test_property_any_shape_transport_kill(hostsim, oracle, algo, p, count, dtype, op, transport, kill, seed):
+    """Any rank count, ragged length, dtype, op, transport and (optionally) one kill point:
+    the outcome class and every survivor's bits equal the oracle's (floats carry NaN /
+    signed zeros / infinities, so MAX / MIN pin the operand order)."""
+    ins = oracle.random_inputs(p, count, seed=seed, dtype=dtype)
+    if dtype in (np.float32, np.float64):
+        ins = H.with_specials(ins, p + 2)
+    kills = []
+    if kill is not None and kill[0] < p:
+        kills = [kill]
+        o = _fn(oracle, algo)(ins, kills, op=op)
+        if not o.aborted and o.status[kill[0]] != oracle.DEAD:
+            kills = []  # a point this schedule never reaches at this p
+    _cmp(_fn(oracle, algo), algo, ins, kills, op=op, env=TRANSPORTS[transport])
