@@ -591,3 +591,48 @@ def test_property_any_shape_transport_kill(hostsim, oracle, algo, p, count, dtyp
         if not o.aborted and o.status[kill[0]] != oracle.DEAD:
             kills = []  # a point this schedule never reaches at this p
     _cmp(_fn(oracle, algo), algo, ins, kills, op=op, env=TRANSPORTS[transport])
+
+
+@settings(max_examples=int(os.environ.get("FTAR_PROPERTY_EXAMPLES", "120")) // 2, deadline=None,
+          suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(algo=st.sampled_from(["raben", "rd"]), p=st.integers(2, 13), count=st.integers(1, 2000),
+       dtype=st.sampled_from([np.float32, np.int32]), op=st.integers(0, 3),
+       transport=st.integers(0, len(TRANSPORTS) - 1), iters=st.integers(1, 3),
+       kills=st.lists(st.tuples(st.integers(0, 12), st.integers(0, 3), st.integers(0, 3), st.integers(0, 3)),
+                      max_size=3, unique_by=lambda k: k[0]),
+       seed=st.integers(0, 10 ** 6))
+def test_property_multi_kill_repeated_calls(hostsim, oracle, algo, p, count, dtype, op, transport, iters, kills,
+                                            seed):
+    """Up to three deaths in the first call, then more calls on the re-targeted comm:
+    call 0 as the oracle's faulty run, every later call as the oracle's fault-free run
+    over the survivors in their new order."""
+    fn = _fn(oracle, algo)
+    ins = oracle.random_inputs(p, count, seed=seed, dtype=dtype)
+    if dtype == np.float32:
+        ins = H.with_specials(ins, p + 2)
+    ks = [k for k in kills if k[0] < p]
+    while True:  # keep the kill points call 0 reaches (an unreached one would fire in a later call)
+        o1 = fn(ins, ks, op=op)
+        if o1.aborted:
+            break
+        reached = [k for k in ks if o1.status[k[0]] == O.DEAD]
+        if reached == ks:
+            break
+        ks = reached
+    if all(s == O.DEAD for s in o1.status):
+        return
+    r = H.run_probe(algo, ins, ks, op=op, iters=iters, backend="hostsim", timeout=120, env_extra=TRANSPORTS[transport])
+    if o1.aborted:
+        assert r.aborted and not r.outputs, (ks, r.stderr[-1000:])
+        return
+    assert not r.aborted and r.returncode == 0, (ks, r.stderr[-1000:])
+    u = {4: np.uint32, 8: np.uint64}[ins[0].dtype.itemsize]
+    o2 = fn([ins[w] for w in o1.order_after], op=op) if iters > 1 else None
+    for w, s in enumerate(o1.status):
+        if s != 0:
+            assert w not in r.outputs
+            continue
+        assert np.array_equal(r.outputs[w][0].view(u), o1.outputs[w].view(u)), (ks, w)
+        for it in range(1, iters):
+            i = o1.order_after.index(w)
+            assert np.array_equal(r.outputs[w][it].view(u), o2.outputs[i].view(u)), (ks, w, it)
