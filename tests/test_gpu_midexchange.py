@@ -211,3 +211,63 @@ def test_random_two_kills_gpu(oracle, seed):
             continue  # a point the schedule never reaches
         _check(fn, algo, ins, kills, op=2)
         n += 1
+
+
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+GPU_TRANSPORTS = [{}, {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}, {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"},
+                  {"FTAR_EXPORT": "0"}, {"FTAR_ONESHOT_MAX": "0"}, {"FTAR_REDUNDANCY": "1", "FTAR_MESH": "0"}]
+
+
+@pytest.mark.timeout(900)
+@settings(max_examples=int(os.environ.get("FTAR_GPU_PROPERTY_EXAMPLES", "20")), deadline=None,
+          suppress_health_check=[HealthCheck.function_scoped_fixture], database=None)
+@given(algo=st.sampled_from(["raben", "rd"]), p=st.integers(2, 8), count=st.integers(1, 300000),
+       op=st.integers(0, 3), transport=st.integers(0, len(GPU_TRANSPORTS) - 1), iters=st.integers(1, 2),
+       kills=st.lists(st.tuples(st.integers(0, 7), st.integers(0, 3), st.integers(0, 3), st.integers(0, 3)),
+                      max_size=2, unique_by=lambda k: k[0]),
+       seed=st.integers(0, 10 ** 6))
+def test_property_gpu(oracle, algo, p, count, op, transport, iters, kills, seed):
+    """The host-sim property test on the GPU: any rank count 2-8, ragged length up to
+    300k float32 (NaN / signed zeros / infinities), op, transport and up to two kill
+    points in call 0, then a second call on the re-targeted comm; outcome and bits as the
+    oracle's."""
+    import oracle as O
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    ins = H.with_specials(oracle.random_inputs(p, count, seed=seed), p + 2)
+    ks = [k for k in kills if k[0] < p]
+    while True:
+        o1 = fn(ins, ks, op=op)
+        if o1.aborted:
+            break
+        reached = [k for k in ks if o1.status[k[0]] == O.DEAD]
+        if reached == ks:
+            break
+        ks = reached
+    r = H.run_probe(algo, ins, ks, op=op, iters=iters, backend="gpu", devmap=ALL_ON_GPU0, timeout=300,
+                    env_extra=GPU_TRANSPORTS[transport])
+    if o1.aborted:
+        assert r.aborted and not r.outputs, (ks, r.stderr[-2000:])
+        return
+    assert not r.aborted and r.returncode == 0, (ks, r.stderr[-2000:])
+    o2 = fn([ins[w] for w in o1.order_after], op=op) if iters > 1 else None
+    for w, s in enumerate(o1.status):
+        if s != 0:
+            assert w not in r.outputs
+            continue
+        assert _same(r.outputs[w][0], o1.outputs[w], op), (ks, w)
+        for it in range(1, iters):
+            i = o1.order_after.index(w)
+            assert _same(r.outputs[w][it], o2.outputs[i], op), (ks, w, it)
+
+
+def _same(got, want, op):
+    """Bit equality; for SUM / PROD a NaN matches any NaN.  When both operands of an add
+    or multiply are NaN, IEEE 754 (6.2.3) leaves open which payload (and sign) the result
+    carries, and compilers swap the operands of commutative ops freely -- the oracle's gcc
+    and the kernels' hipcc pick differently (inf + -inf then NaN + NaN).  MAX / MIN select
+    an operand and stay bit-exact."""
+    if op >= 2:
+        return np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    gn, wn = np.isnan(got), np.isnan(want)
+    return np.array_equal(gn, wn) and np.array_equal(got[~gn].view(np.uint32), want[~wn].view(np.uint32))
