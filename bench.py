@@ -249,7 +249,7 @@ def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
             e["FTAR_KILL"] = kill
         t0 = time.time()
         cp = subprocess.run([ftrun, "-np", str(ranks), "--devmap", ",".join(map(str, devmap)), exe, "raben",
-                             str(count), str(calls)], env=e, capture_output=True, text=True, timeout=600)
+                             str(count), str(calls)], env=e, capture_output=True, text=True, timeout=180)
         lines = [json.loads(l) for l in cp.stdout.splitlines() if l.startswith("{")]
         per_call = []
         for c in range(calls):
@@ -309,6 +309,7 @@ def c5_random_kill(ftrun, exe, ranks, devmap, count, env, calls=3, loop_s=1.5, s
     delay = rng.uniform(1.0, 1.0 + loop_s * calls)  # after the launch: ~1 s of process start-up
     e = dict(env, FTAR_LOOP_SECONDS=str(loop_s))
     out = {"victim": victim, "delay_s": round(delay, 3), "loop_seconds": loop_s, "calls": calls}
+    pr = None
     try:
         import psutil
         t0 = time.time()
@@ -322,10 +323,13 @@ def c5_random_kill(ftrun, exe, ranks, devmap, count, env, calls=3, loop_s=1.5, s
                     out["killed"] = True
             except (psutil.Error, OSError):
                 pass
-        so, se = pr.communicate(timeout=300)
+        so, se = pr.communicate(timeout=180)
         out["job_wall_s"] = round(time.time() - t0, 2)
     except Exception as ex:
         out["error"] = str(ex)[-300:]
+        if pr is not None and pr.poll() is None:
+            pr.kill()  # ftrun's ranks follow it (PR_SET_PDEATHSIG)
+            pr.wait()
         return out
     lines = [json.loads(l) for l in so.splitlines() if l.startswith("{")]
     full = float(sum(range(ranks)))
@@ -353,20 +357,90 @@ def c5_random_kill(ftrun, exe, ranks, devmap, count, env, calls=3, loop_s=1.5, s
     return out
 
 
+def leg_flag(tag):
+    """Flag file rank 0 writes when a rank-0 leg ends (one per torchrun job: its master
+    port and agent pid)."""
+    return os.path.join("/tmp", f"ftar-bench-{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}-{tag}")
+
+
+def side_legs(args, rank, world, devices, rehearsal):
+    """The legs rank 0 runs as other processes -- the CPU baseline (host processes), the
+    configs[4] jobs (ftrun, 9 ranks) and the fabric probe (one process on every GPU) --
+    BEFORE any torchrun rank touches a GPU: the other ranks wait here on a flag file
+    without having imported torch.  Run after the main legs they would share the cards
+    with the job's own ranks (8 + 9 GPU processes at N = 8, beyond what a box lets one
+    job run on a card).  Returns (cpu, c5, xgmi) on rank 0, Nones elsewhere."""
+    flag = leg_flag("side")
+    if rank != 0:
+        while not os.path.exists(flag):
+            time.sleep(0.05)
+        return None, None, None
+    S = args.count * 4
+    cpu = c5 = xgmi = None
+    try:
+        if not args.no_cpu_baseline:
+            # the same schedule on this node's host cores, float32, 256 MiB per rank
+            try:
+                r, model = cpu_schedule("raben", world, args.count, 3)
+                cpu = {"value": round(world * S / r["time_s"] / 1e9, 4), "unit": "GB/s", "cores": world,
+                       "kind": "port", "cpu_model": model, "ms_per_call": round(r["time_s"] * 1e3, 2),
+                       "algbw_GBps": r["algbw_GBps"],
+                       # the reference's TIME is clock() of one rank: CPU seconds per rank
+                       # process (ranks spin, so it tracks wall time; it also covers init,
+                       # fill, checksum)
+                       "cpu_s_per_rank_process": r["cpu_s_per_rank_whole_process"],
+                       "sample": f"Rabenseifner (FT, the reference's step-by-step pairwise shape), {world} rank "
+                                 f"processes pinned one per core, 256 MiB float32 per rank through shared memory, "
+                                 f"median of 3 calls (driver Time: lines, max over ranks); value = {world} x 256 MiB "
+                                 f"/ call time"}
+            except Exception as e:
+                cpu = {"value": None, "unit": "GB/s", "cores": world, "kind": "port",
+                       "sample": f"failed: {str(e)[-300:]}"}
+        if not args.no_c5:
+            # configs[4]: N GPUs' worth of ranks + the idle spare, its own ftrun jobs
+            try:
+                c5 = c5_leg(world, devices, args.count, int(os.environ.get("FTAR_C5_RANKS", "9")))
+            except Exception as e:
+                c5 = {"error": str(e)[-500:]}
+        if not args.no_xgmi:
+            # the fabric (tools/xgmi_probe.hip, one process driving the job's GPUs): one
+            # link one way and both ways (SURVEY.md 8d's B_link), pull vs push, copy
+            # engines, the mesh's all-peers pattern; loopback in a one-GPU rehearsal
+            exe = os.path.join(ROOT, "tools", "_build", "xgmi_probe")
+            try:
+                cp = subprocess.run([exe, str(1 if rehearsal else world)], capture_output=True, text=True,
+                                    timeout=240)
+                lines = [ln for ln in cp.stdout.splitlines() if ln.startswith("{")]
+                xgmi = json.loads(lines[-1]) if lines else {"error": (cp.stderr or cp.stdout)[-300:],
+                                                            "rc": cp.returncode}
+            except Exception as e:
+                xgmi = {"error": str(e)[-300:]}
+    finally:
+        with open(flag, "w") as f:
+            f.write("done")
+    return cpu, c5, xgmi
+
+
 def multi(args):
-    import torch
-    import torch.distributed as dist
-    ftar = load_package()
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     # FTAR_DEVICE pins every rank to one GPU (single-GPU rehearsal of the multi-rank path;
     # RCCL refuses two ranks on one device, so such runs use --dist-backend gloo)
     rehearsal = "FTAR_DEVICE" in os.environ  # every rank on one GPU
+    # this job's GPUs (LOCAL_RANK = GPU on one node), or the one GPU of a rehearsal
+    devices = [int(os.environ["FTAR_DEVICE"])] if rehearsal else list(range(world))
+    cpu, c5, xgmi = side_legs(args, rank, world, devices, rehearsal)
+    import torch
+    import torch.distributed as dist
+    ftar = load_package()
     dev = int(os.environ.get("FTAR_DEVICE", local)) % max(1, torch.cuda.device_count())
     os.environ.setdefault("FTAR_DEVICE", str(dev))  # the library opens the same device
     torch.cuda.set_device(dev)
     dist.init_process_group(backend=args.dist_backend)
+    dist.barrier()
+    if rank == 0:
+        os.unlink(leg_flag("side"))  # every rank is past side_legs
     comm = ftar.Comm.from_env()
     comm.set_profiling(False)  # kernel events only in the profiled passes (timed_split)
     g = torch.Generator(device="cuda").manual_seed(1000 + rank)
@@ -579,71 +653,6 @@ def multi(args):
         zz = x.clone()
         t_nc, _ = timed(lambda: dist.all_reduce(zz))
 
-    def rank0_leg(tag, fn):
-        """fn() on rank 0 while the other ranks SLEEP: a torch.distributed barrier can
-        spin host threads, and the leg pins its own processes to cores.  Rank 0 signals
-        the end through a file; one barrier on each side."""
-        flag = os.path.join("/tmp", f"ftar-bench-{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}-{tag}")
-        dist.barrier()
-        res = None
-        if rank == 0:
-            try:
-                res = fn()
-            finally:
-                with open(flag, "w") as f:
-                    f.write("done")
-        else:
-            while not os.path.exists(flag):
-                time.sleep(0.05)
-        dist.barrier()
-        if rank == 0:
-            os.unlink(flag)
-        return res
-
-    # The CPU baseline: the same schedule on this node's host cores, in this job, rank 0
-    # only (the others sleep), float32, the same 256 MiB per rank.
-    def cpu_leg():
-        try:
-            r, model = cpu_schedule("raben", world, args.count, 3)
-            return {"value": round(world * S / r["time_s"] / 1e9, 4), "unit": "GB/s", "cores": world, "kind": "port",
-                   "cpu_model": model, "ms_per_call": round(r["time_s"] * 1e3, 2), "algbw_GBps": r["algbw_GBps"],
-                   # the reference's TIME is clock() of one rank: CPU seconds per rank process
-                   # (ranks spin, so it tracks wall time; it also covers init, fill, checksum)
-                   "cpu_s_per_rank_process": r["cpu_s_per_rank_whole_process"],
-                   "sample": f"Rabenseifner (FT, the reference's step-by-step pairwise shape), {world} rank processes "
-                             f"pinned one per core, 256 MiB float32 per rank through shared memory, median of 3 "
-                             f"calls (driver Time: lines, max over ranks); value = {world} x 256 MiB / call time"}
-        except Exception as e:
-            return {"value": None, "unit": "GB/s", "cores": world, "kind": "port", "sample": f"failed: {str(e)[-300:]}"}
-
-    cpu = None if args.no_cpu_baseline else rank0_leg("cpu", cpu_leg)
-
-    # configs[4]: the single-kill leg, its own ftrun job (rank 0), after everything else
-    def c5_run():
-        # this job's GPUs (LOCAL_RANK = GPU on one node), or the one GPU of a rehearsal
-        devices = [dev] if rehearsal else list(range(world))
-        try:
-            return c5_leg(world, devices, args.count, int(os.environ.get("FTAR_C5_RANKS", "9")))
-        except Exception as e:
-            return {"error": str(e)[-500:]}
-
-    c5 = None if args.no_c5 else rank0_leg("c5", c5_run)
-
-    # The fabric itself (tools/xgmi_probe.hip, one process driving the job's GPUs): one
-    # link one way and both ways (SURVEY.md 8d's B_link), pull vs push, copy engines, and
-    # the all-peers pattern of the mesh.  A one-GPU rehearsal runs it in loopback.
-    def xgmi_leg():
-        exe = os.path.join(ROOT, "tools", "_build", "xgmi_probe")
-        try:
-            cp = subprocess.run([exe, str(1 if rehearsal else world)], capture_output=True, text=True, timeout=240)
-            lines = [ln for ln in cp.stdout.splitlines() if ln.startswith("{")]
-            if lines:
-                return json.loads(lines[-1])
-            return {"error": (cp.stderr or cp.stdout)[-300:], "rc": cp.returncode}
-        except Exception as e:
-            return {"error": str(e)[-300:]}
-
-    xgmi = None if args.no_xgmi else rank0_leg("xgmi", xgmi_leg)
     L = world.bit_length() - 1
     r = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
     # Link bytes per rank per direction (SURVEY.md 8d).  The reference's FT Raben moves
