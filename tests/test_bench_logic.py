@@ -95,3 +95,40 @@ def test_c5_leg_wrong_sum_is_not_recovered(bench, monkeypatch):
     res = m.c5_leg(8, list(range(8)), 1024, 9)
     assert res["recovered"] is False
     assert not all(c["result_ok"] for c in res["fault"]["calls"])
+
+
+def test_side_legs_run_on_rank0_before_torch(bench, monkeypatch):
+    """The side legs (CPU baseline, configs[4] jobs, fabric probe) run on rank 0 only, and
+    rank 0 writes the flag the other ranks wait on even when a leg raises; the other
+    ranks return as soon as the flag exists.  Neither imports torch (the ranks are not
+    GPU processes while the legs run: tools/kfd_probe.py)."""
+    import argparse
+    import sys
+    m, tmp = bench
+    monkeypatch.setenv("MASTER_PORT", f"t{os.getpid()}")
+    calls = []
+
+    def c5(world, devices, count, ranks):
+        calls.append((world, devices, count, ranks))
+        raise RuntimeError("leg failed")
+
+    monkeypatch.setattr(m, "c5_leg", c5)
+    monkeypatch.setattr(m, "cpu_schedule", lambda *a: (_ for _ in ()).throw(OSError("no cores")))
+    monkeypatch.setenv("FTAR_C5_RANKS", "9")
+    args = argparse.Namespace(count=1 << 10, no_cpu_baseline=False, no_c5=False, no_xgmi=True)
+    had_torch = "torch" in sys.modules
+    flag = m.leg_flag("side")
+    assert not os.path.exists(flag)
+    try:
+        cpu, c5r, xg = m.side_legs(args, 0, 8, list(range(8)), False)
+        assert os.path.exists(flag)
+        assert calls == [(8, list(range(8)), 1 << 10, 9)]
+        assert c5r == {"error": "leg failed"} and xg is None
+        assert cpu["value"] is None and "no cores" in cpu["sample"] and cpu["cores"] == 8
+        assert m.side_legs(args, 3, 8, list(range(8)), False) == (None, None, None)
+        assert len(calls) == 1
+        if not had_torch:
+            assert "torch" not in sys.modules
+    finally:
+        if os.path.exists(flag):
+            os.unlink(flag)
