@@ -604,6 +604,59 @@ def multi(args):
             if tv_rd:
                 transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
         set_opts([chosen_opts[o] for o in opts])
+    # Exactness on this node's GPUs, every transport: integer-valued float32 inputs that
+    # change from trial to trial (so a stale cached line or a read of the previous call's
+    # window cannot pass), where every partial sum is an integer below 2^24 and hence
+    # exact in any order.  Each rank regenerates every rank's input from its seed and sums
+    # them itself: the expected result needs no collective.  Trials reuse the same buffers
+    # (the peers' mappings of our send buffer are reused too).
+    xe = torch.empty(args.count, device="cuda")
+    ye = torch.empty_like(xe)
+    want = torch.empty_like(xe)
+
+    def int_input(out, trial, r, n):
+        ge = torch.Generator(device="cuda").manual_seed(7919 * trial + r)
+        out[:n].copy_(torch.randint(-1024, 1024, (n,), device="cuda", generator=ge, dtype=torch.int32))
+
+    def exact_ok(fn, trials=(1, 2), n=None):
+        n = args.count if n is None else n
+        bad = 0
+        for t in trials:
+            int_input(xe, t, rank, n)
+            want[:n].zero_()
+            for r in range(world):
+                int_input(ye, t, r, n)
+                want[:n] += ye[:n]
+            ye.fill_(float("nan"))
+            if fn(xe, ye, count=n) != 0 or not torch.equal(ye[:n], want[:n]):
+                bad += 1
+        return bad
+
+    checks = [("chosen", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, None),
+              ("reference_shape", (0, 0, 0, 1, 0), comm.allreduce_rabenseifner, None),
+              ("rd", [chosen_opts[o] for o in opts], comm.recursive_doubling, None),
+              ("chosen_64KiB", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, 16384)]
+    if not args.no_variants:
+        checks += [(name, vals, comm.allreduce_rabenseifner, None) for name, vals in
+                   (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
+                    ("copy_engine", (0, 1, 1, 0, 0))) if pow2 or name != "mesh"]
+        checks += [("rd_relay", (1, 1, 0, 0, 0), comm.recursive_doubling, None),
+                   ("rd_direct", (0, 1, 0, 0, 0), comm.recursive_doubling, None)]
+    comm.set_profiling(False)
+    fails = []
+    for name, vals, fn, n in checks:
+        set_opts(vals)
+        if name == "rd" and rd_selection:  # the transport the RD timing chose
+            comm.set_option(ftar.OPT_RELAY, int(rd_selection["chosen"] == "relay2hop"))
+        fails.append(exact_ok(fn, n=n))
+    set_opts([chosen_opts[o] for o in opts])
+    comm.set_profiling(True)
+    fails = max_over_ranks(fails)
+    exact = {"inputs": "integer-valued float32 in [-1024, 1024), new per trial, 2 trials per transport; expected "
+                       "sum regenerated on every rank (exact in any order)",
+             "all_exact": all(f == 0 for f in fails)}
+    exact.update({name: f == 0 for (name, _, _, _), f in zip(checks, fails)})
+    del xe, ye, want
     # Per-call time over message sizes (max over ranks), 4 B .. 256 MiB, with the chosen
     # transport, next to RCCL's all_reduce on the same sizes: the FT/vendor curve of the
     # reference's compare campaign (slurm/test_compare.slurm:27-50, check_compare.py),
@@ -774,6 +827,7 @@ def multi(args):
             "size_sweep_us": sizes,
             "max_abs_err_vs_rccl": err,
             "int32_rank_checksum_ok": {"raben": cks_raben == cks_want, "rd": cks_rd == cks_want},
+            "exact_on_node": exact,
             "c5_single_kill": c5,
             "cpu_baseline": cpu,
         }

@@ -58,6 +58,8 @@ def test_bench_two_rank_scale_path():
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["int32_rank_checksum_ok"] == {"raben": True, "rd": True}
     assert d["max_abs_err_vs_rccl"] < 1e-5
+    ex = d["exact_on_node"]  # integer-valued float inputs, new per trial: bitwise exact
+    assert ex["all_exact"] and ex["chosen"] and ex["reference_shape"] and ex["rd"] and ex["chosen_64KiB"], ex
     assert d["config"]["schedule"] and d["config"]["transport"] == d["transport"]
     assert d["reference_shape"]["ms_per_step"] > 0
     cpu = d["cpu_baseline"]
