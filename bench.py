@@ -512,6 +512,34 @@ def multi(args):
         for o, v in zip(opts, vals):
             comm.set_option(o, v)
 
+    # Exactness on this node's GPUs, every transport: integer-valued float32 inputs that
+    # change from trial to trial (so a stale cached line or a read of the previous call's
+    # window cannot pass), where every partial sum is an integer below 2^24 and hence
+    # exact in any order.  Each rank regenerates every rank's input from its seed and sums
+    # them itself: the expected result needs no collective.  Trials reuse the same buffers
+    # (the peers' mappings of our send buffer are reused too).
+    xe = torch.empty(args.count, device="cuda")
+    ye = torch.empty_like(xe)
+    want = torch.empty_like(xe)
+
+    def int_input(out, trial, r, n):
+        ge = torch.Generator(device="cuda").manual_seed(7919 * trial + r)
+        out[:n].copy_(torch.randint(-1024, 1024, (n,), device="cuda", generator=ge, dtype=torch.int32))
+
+    def exact_ok(fn, trials=(1, 2), n=None):
+        n = args.count if n is None else n
+        bad = 0
+        for t in trials:
+            int_input(xe, t, rank, n)
+            want[:n].zero_()
+            for r in range(world):
+                int_input(ye, t, r, n)
+                want[:n] += ye[:n]
+            ye.fill_(float("nan"))
+            if fn(xe, ye, count=n) != 0 or not torch.equal(ye[:n], want[:n]):
+                bad += 1
+        return bad
+
     # Transport selection before the timed run: how the node's xGMI links behave under
     # concurrent peer reads decides between the one-hop mesh (power-of-two p without a
     # spare), the 2-hop relay and plain pairwise pulls, so a short comparison (max over
@@ -526,16 +554,26 @@ def multi(args):
             cands["relay2hop"] = (0, 1)
         cands["direct"] = (0, 0)
         if len(cands) > 1:
-            times = {}
+            times, inexact = {}, []
             for name, (m, r) in cands.items():
                 comm.set_option(ftar.OPT_MESH, m)
                 comm.set_option(ftar.OPT_RELAY, r)
+                # a transport that is not bit-exact on this node never times the headline
+                if max_over_ranks([exact_ok(comm.allreduce_rabenseifner, trials=(0,))])[0]:
+                    inexact.append(name)
+                    continue
                 times[name] = quick(raben)
-            chosen = min(times, key=times.get)
-            comm.set_option(ftar.OPT_MESH, cands[chosen][0])
-            comm.set_option(ftar.OPT_RELAY, cands[chosen][1])
+            if times:
+                chosen = min(times, key=times.get)
+                comm.set_option(ftar.OPT_MESH, cands[chosen][0])
+                comm.set_option(ftar.OPT_RELAY, cands[chosen][1])
+            else:  # every one failed: keep the defaults, exact_on_node reports it
+                chosen = None
+                comm.set_option(ftar.OPT_MESH, defaults[ftar.OPT_MESH])
+                comm.set_option(ftar.OPT_RELAY, defaults[ftar.OPT_RELAY])
             selection = {f"{k}_ms": round(t * 1e3, 4) for k, t in times.items()}
             selection["chosen"] = chosen
+            selection["inexact"] = inexact
 
     t_rb, k_rb = timed_split(raben)
     step0_bytes = timed.link_bytes
@@ -604,34 +642,7 @@ def multi(args):
             if tv_rd:
                 transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
         set_opts([chosen_opts[o] for o in opts])
-    # Exactness on this node's GPUs, every transport: integer-valued float32 inputs that
-    # change from trial to trial (so a stale cached line or a read of the previous call's
-    # window cannot pass), where every partial sum is an integer below 2^24 and hence
-    # exact in any order.  Each rank regenerates every rank's input from its seed and sums
-    # them itself: the expected result needs no collective.  Trials reuse the same buffers
-    # (the peers' mappings of our send buffer are reused too).
-    xe = torch.empty(args.count, device="cuda")
-    ye = torch.empty_like(xe)
-    want = torch.empty_like(xe)
-
-    def int_input(out, trial, r, n):
-        ge = torch.Generator(device="cuda").manual_seed(7919 * trial + r)
-        out[:n].copy_(torch.randint(-1024, 1024, (n,), device="cuda", generator=ge, dtype=torch.int32))
-
-    def exact_ok(fn, trials=(1, 2), n=None):
-        n = args.count if n is None else n
-        bad = 0
-        for t in trials:
-            int_input(xe, t, rank, n)
-            want[:n].zero_()
-            for r in range(world):
-                int_input(ye, t, r, n)
-                want[:n] += ye[:n]
-            ye.fill_(float("nan"))
-            if fn(xe, ye, count=n) != 0 or not torch.equal(ye[:n], want[:n]):
-                bad += 1
-        return bad
-
+    # Exactness of every transport on this node (helpers above the selection)
     checks = [("chosen", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, None),
               ("reference_shape", (0, 0, 0, 1, 0), comm.allreduce_rabenseifner, None),
               ("rd", [chosen_opts[o] for o in opts], comm.recursive_doubling, None),
