@@ -215,33 +215,9 @@ def e2e_local(ftar, count, iters=5):
         ts["h2d"] += t1 - t0
         ts["d2h"] += t3 - t2
         ts["total"] += t3 - t0
-    # chunk pipeline: chunk k's H2D, chunk k-1's reduce and chunk k-2's D2H in flight at
-    # once on three streams (PCIe is full duplex; the kernel needs ~0.5 % of the time)
-    chunk = 1 << 22
-    sh, sk, sd = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
-    nchunks = (count + chunk - 1) // chunk
-    tp = 0.0
-    for _ in range(iters):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(nchunks):
-            c = slice(i * chunk, min(count, (i + 1) * chunk))
-            with torch.cuda.stream(sh):
-                xd[c].copy_(xh[c], non_blocking=True)
-                yd[c].copy_(yh[c], non_blocking=True)
-            sk.wait_stream(sh)
-            with torch.cuda.stream(sk):
-                ftar.reduce_local(xd[c], yd[c])
-            sd.wait_stream(sk)
-            with torch.cuda.stream(sd):
-                yh[c].copy_(yd[c], non_blocking=True)
-        torch.cuda.synchronize()
-        tp += time.perf_counter() - t0
     return {"h2d_GBps": round(2 * S * iters / ts["h2d"] / 1e9, 2), "d2h_GBps": round(S * iters / ts["d2h"] / 1e9, 2),
             "ms": round(ts["total"] * 1e3 / iters, 3),
-            "GBps": round(2 * S * iters / ts["total"] / 1e9, 2),
-            "pipelined": {"chunk_MiB": chunk * 4 >> 20, "ms": round(tp * 1e3 / iters, 3),
-                          "GBps": round(2 * S * iters / tp / 1e9, 2)}}
+            "GBps": round(2 * S * iters / ts["total"] / 1e9, 2)}
 
 
 def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
