@@ -22,11 +22,13 @@ LIB_PATH = os.path.join(HERE, "lib", "libftar.so")
 
 INT32, FLOAT32, INT64, FLOAT64 = 0, 1, 2, 3
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
+LAND, BAND, LOR, BOR, LXOR, BXOR = 4, 5, 6, 7, 8, 9  # MPI logical / bitwise ops (integer types)
 PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
 PT_BEFORE, PT_AFTER, PT_BARRIER, PT_DURING = 0, 1, 2, 3
 OPT_OVERLAP, OPT_RELAY, OPT_RELAY_MIN, OPT_LOOP_SECONDS, OPT_COPY_ENGINE, OPT_REDUNDANCY, OPT_MESH = 0, 1, 2, 3, 4, 5, 6
 OPT_ONESHOT_MAX = 7
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
+ERR_OP = 9  # MPI_ERR_OP: a logical / bitwise op on a float type
 
 
 class FtarError(RuntimeError):

@@ -38,6 +38,15 @@ size_t ftar_esize(int dtype)
     }
 }
 
+/* MPI_Reduce_local's type/op check: an unknown type or op is an argument error, a
+ * logical or bitwise op on a floating-point type is MPI_ERR_OP (MPI 4.1, 6.9.2). */
+int ftar_check_op(int dtype, int op)
+{
+    if (ftar_esize(dtype) == 0 || op < FTAR_SUM || op >= FTAR_NOPS) return FTAR_ERR_ARG;
+    if (op >= FTAR_LAND && (dtype == FTAR_FLOAT32 || dtype == FTAR_FLOAT64)) return FTAR_ERR_OP;
+    return FTAR_SUCCESS;
+}
+
 int ftar_hibit(int value, int start) /* raben/util.c:22-37 */
 {
     unsigned int mask = (unsigned int)value & ((1u << start) - 1u);
@@ -691,9 +700,10 @@ int ftar_set_profiling(ftar_comm *c, int on)
 
 int ftar_reduce_local(const void *in, void *inout, size_t count, ftar_dtype dtype, ftar_op op, void *stream)
 {
-    if (ftar_esize(dtype) == 0 || op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
+    int rc = ftar_check_op((int)dtype, (int)op);
+    if (rc) return rc;
     if (count && (!in || !inout)) return FTAR_ERR_ARG;
-    int rc = fdev_reduce_local(in, inout, count, (int)dtype, (int)op, stream);
+    rc = fdev_reduce_local(in, inout, count, (int)dtype, (int)op, stream);
     if (rc) fprintf(stderr, "ftar_reduce_local: %s\n", fdev_last_error());
     return rc;
 }

@@ -329,7 +329,7 @@ static hipEvent_t get_event(ftar_dev *d)
 static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     size_t es = esize_of(dtype);
-    if (es == 0 || op < 0 || op > 3 || nseg < 0 || nseg > FDEV_MAX_SEGS || tag < 0 || tag >= FDEV_NTAGS) {
+    if (es == 0 || op < 0 || op >= ftar::kNumOps || nseg < 0 || nseg > FDEV_MAX_SEGS || tag < 0 || tag >= FDEV_NTAGS) {
         snprintf(g_err, sizeof(g_err), "fdev_run: bad arguments");
         return 13;
     }
@@ -371,7 +371,7 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
               size_t n, int tag)
 {
     size_t es = esize_of(dtype);
-    if (es == 0 || op < 0 || op > 3 || tag < 0 || tag >= FDEV_NTAGS ||
+    if (es == 0 || op < 0 || op >= ftar::kNumOps || tag < 0 || tag >= FDEV_NTAGS ||
         !(nsrc == 2 || nsrc == 4 || nsrc == 8 || nsrc == 16)) {
         snprintf(g_err, sizeof(g_err), "fdev_tree: bad arguments");
         return 13;
@@ -414,7 +414,7 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
                     void *const *out, const size_t *n, int ntree, int tag)
 {
     size_t es = esize_of(dtype);
-    if (es == 0 || op < 0 || op > 3 || tag < 0 || tag >= FDEV_NTAGS || ntree < 1 || ntree > ftar::kMaxBatch ||
+    if (es == 0 || op < 0 || op >= ftar::kNumOps || tag < 0 || tag >= FDEV_NTAGS || ntree < 1 || ntree > ftar::kMaxBatch ||
         !(nsrc == 2 || nsrc == 4 || nsrc == 8)) {
         snprintf(g_err, sizeof(g_err), "fdev_tree_batch: bad arguments");
         return 13;
@@ -686,7 +686,7 @@ int fdev_set_reduce_variant(int v)
 int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream)
 {
     size_t es = esize_of(dtype);
-    if (es == 0 || op < 0 || op > 3) {
+    if (es == 0 || op < 0 || op >= ftar::kNumOps) {
         snprintf(g_err, sizeof(g_err), "reduce_local: bad dtype/op");
         return 13;
     }

@@ -87,6 +87,7 @@ struct ftar_comm {
 };
 
 size_t ftar_esize(int dtype);
+int ftar_check_op(int dtype, int op);
 int ftar_my_comm_rank(const ftar_comm *c);
 int ftar_comm_rank_of(const ftar_comm *c, int w);
 

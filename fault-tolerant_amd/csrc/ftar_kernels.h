@@ -7,7 +7,8 @@
 namespace ftar {
 
 enum { kInt32 = 0, kFloat32 = 1, kInt64 = 2, kFloat64 = 3 };
-enum { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
+enum { kSum = 0, kProd = 1, kMax = 2, kMin = 3, kLand = 4, kBand = 5, kLor = 6, kBor = 7, kLxor = 8, kBxor = 9 };
+constexpr int kNumOps = 10; // logical / bitwise ops (>= kLand) exist for the integer types only
 enum { kCopy = 0, kReduce = 1 };
 
 constexpr int kMaxKSegs = 48; // 16 user segments x (head, body, tail); 2.3 KB of kernarg

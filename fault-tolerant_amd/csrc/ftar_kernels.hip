@@ -26,6 +26,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "ftar_kernels.h"
 
 namespace ftar {
@@ -44,7 +46,42 @@ __device__ __forceinline__ T apply(T x, T y)
     if constexpr (OP == kSum) return (T)((U)x + (U)y);
     else if constexpr (OP == kProd) return (T)((U)x * (U)y);
     else if constexpr (OP == kMax) return (x > y) ? x : y;
-    else return (x < y) ? x : y;
+    else if constexpr (OP == kMin) return (x < y) ? x : y;
+    // MPI's logical and bitwise ops (integer types only; the logical ones give 0 / 1)
+    else if constexpr (OP == kLand) return (T)((x != 0) && (y != 0));
+    else if constexpr (OP == kBand) return (T)(x & y);
+    else if constexpr (OP == kLor) return (T)((x != 0) || (y != 0));
+    else if constexpr (OP == kBor) return (T)(x | y);
+    else if constexpr (OP == kLxor) return (T)((x != 0) != (y != 0));
+    else return (T)(x ^ y);
+}
+
+// Runs fn(std::integral_constant<int, OP>) for the runtime op: one instantiation per op
+// the element type has (the logical / bitwise ops only for the integer types).
+template <typename T, typename Fn>
+static hipError_t with_op(int op, Fn &&fn)
+{
+    using std::integral_constant;
+    constexpr bool integer = std::is_integral<T>::value;
+    switch (op) {
+    case kSum: return fn(integral_constant<int, kSum>{});
+    case kProd: return fn(integral_constant<int, kProd>{});
+    case kMax: return fn(integral_constant<int, kMax>{});
+    case kMin: return fn(integral_constant<int, kMin>{});
+    default: break;
+    }
+    if constexpr (integer) {
+        switch (op) {
+        case kLand: return fn(integral_constant<int, kLand>{});
+        case kBand: return fn(integral_constant<int, kBand>{});
+        case kLor: return fn(integral_constant<int, kLor>{});
+        case kBor: return fn(integral_constant<int, kBor>{});
+        case kLxor: return fn(integral_constant<int, kLxor>{});
+        case kBxor: return fn(integral_constant<int, kBxor>{});
+        default: break;
+        }
+    }
+    return hipErrorInvalidValue;
 }
 
 template <typename T, int OP>
@@ -293,13 +330,7 @@ static hipError_t launch_tree_op(int p, const TreeArgs &A, unsigned grid, hipStr
 template <typename T>
 static hipError_t launch_tree_t(int op, int p, const TreeArgs &A, unsigned grid, hipStream_t s)
 {
-    switch (op) {
-    case kSum: return launch_tree_op<T, kSum>(p, A, grid, s);
-    case kProd: return launch_tree_op<T, kProd>(p, A, grid, s);
-    case kMax: return launch_tree_op<T, kMax>(p, A, grid, s);
-    case kMin: return launch_tree_op<T, kMin>(p, A, grid, s);
-    default: return hipErrorInvalidValue;
-    }
+    return with_op<T>(op, [&](auto o) { return launch_tree_op<T, decltype(o)::value>(p, A, grid, s); });
 }
 
 hipError_t launch_tree(int dtype, int op, int p, const TreeArgs &A, unsigned grid, hipStream_t s)
@@ -340,13 +371,7 @@ static hipError_t launch_batch_op(int p, const TreeBatch &B, unsigned grid, hipS
 template <typename T>
 static hipError_t launch_batch_t(int op, int p, const TreeBatch &B, unsigned grid, hipStream_t s)
 {
-    switch (op) {
-    case kSum: return launch_batch_op<T, kSum>(p, B, grid, s);
-    case kProd: return launch_batch_op<T, kProd>(p, B, grid, s);
-    case kMax: return launch_batch_op<T, kMax>(p, B, grid, s);
-    case kMin: return launch_batch_op<T, kMin>(p, B, grid, s);
-    default: return hipErrorInvalidValue;
-    }
+    return with_op<T>(op, [&](auto o) { return launch_batch_op<T, decltype(o)::value>(p, B, grid, s); });
 }
 
 hipError_t launch_tree_batch(int dtype, int op, int p, const TreeBatch &B, unsigned grid, hipStream_t s)
@@ -363,14 +388,10 @@ hipError_t launch_tree_batch(int dtype, int op, int p, const TreeBatch &B, unsig
 template <typename T>
 static hipError_t launch_t(int op, const KSegList &L, unsigned grid, hipStream_t s)
 {
-    switch (op) {
-    case kSum: hipLaunchKernelGGL((segment_kernel<T, kSum>), dim3(grid), dim3(kBlock), 0, s, L); break;
-    case kProd: hipLaunchKernelGGL((segment_kernel<T, kProd>), dim3(grid), dim3(kBlock), 0, s, L); break;
-    case kMax: hipLaunchKernelGGL((segment_kernel<T, kMax>), dim3(grid), dim3(kBlock), 0, s, L); break;
-    case kMin: hipLaunchKernelGGL((segment_kernel<T, kMin>), dim3(grid), dim3(kBlock), 0, s, L); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+    return with_op<T>(op, [&](auto o) {
+        hipLaunchKernelGGL((segment_kernel<T, decltype(o)::value>), dim3(grid), dim3(kBlock), 0, s, L);
+        return hipGetLastError();
+    });
 }
 
 hipError_t launch_segments(int dtype, int op, const KSegList &L, unsigned grid, hipStream_t s)
@@ -388,14 +409,11 @@ template <typename T>
 static hipError_t launch_lds_t(int op, uint4 *inout, const uint4 *in, size_t nv, unsigned grid, hipStream_t s,
                                unsigned nts)
 {
-    switch (op) {
-    case kSum: hipLaunchKernelGGL((reduce_lds_kernel<T, kSum>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv, nts); break;
-    case kProd: hipLaunchKernelGGL((reduce_lds_kernel<T, kProd>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv, nts); break;
-    case kMax: hipLaunchKernelGGL((reduce_lds_kernel<T, kMax>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv, nts); break;
-    case kMin: hipLaunchKernelGGL((reduce_lds_kernel<T, kMin>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv, nts); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+    return with_op<T>(op, [&](auto o) {
+        hipLaunchKernelGGL((reduce_lds_kernel<T, decltype(o)::value>), dim3(grid), dim3(kBlock), 0, s, inout, in, nv,
+                           nts);
+        return hipGetLastError();
+    });
 }
 
 hipError_t launch_reduce_lds(int dtype, int op, void *inout, const void *in, size_t nvec, unsigned grid,

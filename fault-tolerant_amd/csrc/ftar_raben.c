@@ -425,7 +425,8 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     x->op = (int)op;
     x->es = ftar_esize(dtype);
     x->count = count;
-    if (x->es == 0 || op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
+    int orc = ftar_check_op((int)dtype, (int)op);
+    if (orc) return orc;
     x->steps = ftar_hibit(c->size, (int)(sizeof(int) * 8) - 1); /* :16-21 */
     if (x->steps == -1) return FTAR_ERR_ARG;
     if (count == 0) return FTAR_ERR_UNKNOWN; /* copy_buffer(count <= 0), util.c:40-43 */
@@ -678,8 +679,9 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
                                      ftar_comm *c)
 {
     if (!c) return FTAR_ERR_ARG;
+    int orc = ftar_check_op((int)dtype, (int)op); /* before anything is copied */
+    if (orc) return orc;
     size_t es = ftar_esize(dtype);
-    if (es == 0) return FTAR_ERR_ARG;
     size_t bytes = count * es;
     ftar_ensure_staging(c, bytes);
     /* Power of two without a spare (every failure aborts, so nothing is recovered across

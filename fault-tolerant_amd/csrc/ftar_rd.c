@@ -173,7 +173,8 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     x->op = (int)op;
     x->es = ftar_esize(dtype);
     x->count = count;
-    if (x->es == 0 || op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
+    int orc = ftar_check_op((int)dtype, (int)op);
+    if (orc) return orc;
     if (count && (!src || !dst)) return FTAR_ERR_ARG;
     if (count == 0) return FTAR_SUCCESS;
     /* device pointers: pageable host memory or a short allocation is refused, not faulted on */
@@ -305,8 +306,9 @@ int ftar_recursive_doubling_host(const void *src, void *dst, size_t count, ftar_
                                  ftar_comm *c)
 {
     if (!c) return FTAR_ERR_ARG;
+    int orc = ftar_check_op((int)dtype, (int)op); /* before anything is copied */
+    if (orc) return orc;
     size_t es = ftar_esize(dtype);
-    if (es == 0) return FTAR_ERR_ARG;
     size_t bytes = count * es;
     ftar_ensure_staging(c, bytes);
     if (bytes && fdev_h2d(c->dev, c->hsend, src, bytes)) return FTAR_ERR_DEVICE;

@@ -34,6 +34,7 @@ extern "C" {
 
 /* ---- return codes: the MPI error classes the reference relies on ---------- */
 #define FTAR_SUCCESS         0   /* MPI_SUCCESS */
+#define FTAR_ERR_OP          9   /* MPI_ERR_OP: a bitwise / logical op on a floating-point type */
 #define FTAR_ERR_ARG         13  /* MPI_ERR_ARG      (raben/rabenseifner.c:18-20) */
 #define FTAR_ERR_UNKNOWN     14  /* MPI_ERR_UNKNOWN  (raben/util.c:40-43) */
 #define FTAR_ERR_OTHER       16  /* MPI_ERR_OTHER    (rd/util.c:75) */
@@ -50,12 +51,25 @@ typedef enum {
     FTAR_FLOAT64 = 3
 } ftar_dtype;
 
+/* MPI's predefined reduction ops (MAXLOC / MINLOC need pair types and are not offered).
+ * The reference passes its MPI_Op straight to MPI_Reduce_local (raben/rabenseifner.c:
+ * 86-87,117,234-236; rd/util.c:32; rd/recursive_doubling.c:44,48), so every op MPI
+ * defines for these types is valid there.  As in MPI, the logical and bitwise ops are
+ * defined for the integer types only (FTAR_ERR_OP for a float type); the logical ones
+ * yield 0 or 1. */
 typedef enum {
     FTAR_SUM = 0,  /* MPI_SUM (the only op the reference drivers use) */
     FTAR_PROD = 1,
     FTAR_MAX = 2,
-    FTAR_MIN = 3
+    FTAR_MIN = 3,
+    FTAR_LAND = 4, /* MPI_LAND: (a != 0) && (b != 0) */
+    FTAR_BAND = 5, /* MPI_BAND: a & b */
+    FTAR_LOR = 6,  /* MPI_LOR */
+    FTAR_BOR = 7,  /* MPI_BOR */
+    FTAR_LXOR = 8, /* MPI_LXOR: (a != 0) != (b != 0) */
+    FTAR_BXOR = 9  /* MPI_BXOR */
 } ftar_op;
+#define FTAR_NOPS 10
 
 /* ---- deterministic fault injection --------------------------------------
  * A kill names the victim (original world rank) and the place in the schedule

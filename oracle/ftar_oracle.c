@@ -35,35 +35,73 @@ size_t ftar_oracle_esize(int dtype)
 
 /* OpenMPI's 2-buffer ops compute out = out <op> in, and for MAX/MIN
  * out = (out > in) ? out : in  (ompi/mca/op/base/op_base_functions.c).  The
- * reference only ever uses MPI_SUM; the other ops follow the same operand roles. */
-#define DEF_REDUCE(NAME, T, UT)                                                   \
+ * reference only ever uses MPI_SUM; the other ops follow the same operand roles.
+ * MPI's logical ops (LAND, LOR, LXOR) yield 0 / 1, the bitwise ones (BAND, BOR, BXOR)
+ * act on the two's-complement bits; both exist for the integer types only
+ * (MPI 4.1 section 6.9.2), which ftar_oracle_reduce_local enforces. */
+#define ARITH_CASES(T, UT)                                                        \
+    case FTAR_SUM:                                                                \
+        for (i = 0; i < n; i++) inout[i] = (T)((UT)inout[i] + (UT)in[i]);         \
+        break;                                                                    \
+    case FTAR_PROD:                                                               \
+        for (i = 0; i < n; i++) inout[i] = (T)((UT)inout[i] * (UT)in[i]);         \
+        break;                                                                    \
+    case FTAR_MAX:                                                                \
+        for (i = 0; i < n; i++) inout[i] = (inout[i] > in[i]) ? inout[i] : in[i]; \
+        break;                                                                    \
+    case FTAR_MIN:                                                                \
+        for (i = 0; i < n; i++) inout[i] = (inout[i] < in[i]) ? inout[i] : in[i]; \
+        break;
+#define BIT_CASES(T)                                                              \
+    case FTAR_LAND:                                                               \
+        for (i = 0; i < n; i++) inout[i] = (T)(inout[i] != 0 && in[i] != 0);      \
+        break;                                                                    \
+    case FTAR_BAND:                                                               \
+        for (i = 0; i < n; i++) inout[i] = (T)(inout[i] & in[i]);                 \
+        break;                                                                    \
+    case FTAR_LOR:                                                                \
+        for (i = 0; i < n; i++) inout[i] = (T)(inout[i] != 0 || in[i] != 0);      \
+        break;                                                                    \
+    case FTAR_BOR:                                                                \
+        for (i = 0; i < n; i++) inout[i] = (T)(inout[i] | in[i]);                 \
+        break;                                                                    \
+    case FTAR_LXOR:                                                               \
+        for (i = 0; i < n; i++) inout[i] = (T)((inout[i] != 0) != (in[i] != 0)); \
+        break;                                                                    \
+    case FTAR_BXOR:                                                               \
+        for (i = 0; i < n; i++) inout[i] = (T)(inout[i] ^ in[i]);                 \
+        break;
+#define DEF_REDUCE_INT(NAME, T, UT)                                               \
     static void NAME(int op, const T *in, T *inout, size_t n)                     \
     {                                                                             \
         size_t i;                                                                 \
-        switch (op) {                                                             \
-        case FTAR_SUM:                                                            \
-            for (i = 0; i < n; i++) inout[i] = (T)((UT)inout[i] + (UT)in[i]);     \
-            break;                                                                \
-        case FTAR_PROD:                                                           \
-            for (i = 0; i < n; i++) inout[i] = (T)((UT)inout[i] * (UT)in[i]);     \
-            break;                                                                \
-        case FTAR_MAX:                                                            \
-            for (i = 0; i < n; i++) inout[i] = (inout[i] > in[i]) ? inout[i] : in[i]; \
-            break;                                                                \
-        case FTAR_MIN:                                                            \
-            for (i = 0; i < n; i++) inout[i] = (inout[i] < in[i]) ? inout[i] : in[i]; \
-            break;                                                                \
-        }                                                                         \
+        switch (op) { ARITH_CASES(T, UT) BIT_CASES(T) }                           \
+    }
+#define DEF_REDUCE_FLOAT(NAME, T)                                                 \
+    static void NAME(int op, const T *in, T *inout, size_t n)                     \
+    {                                                                             \
+        size_t i;                                                                 \
+        switch (op) { ARITH_CASES(T, T) }                                         \
     }
 
-DEF_REDUCE(reduce_i32, int32_t, uint32_t)
-DEF_REDUCE(reduce_i64, int64_t, uint64_t)
-DEF_REDUCE(reduce_f32, float, float)
-DEF_REDUCE(reduce_f64, double, double)
+DEF_REDUCE_INT(reduce_i32, int32_t, uint32_t)
+DEF_REDUCE_INT(reduce_i64, int64_t, uint64_t)
+DEF_REDUCE_FLOAT(reduce_f32, float)
+DEF_REDUCE_FLOAT(reduce_f64, double)
+
+/* type/op check of MPI_Reduce_local: unknown -> MPI_ERR_ARG, logical or bitwise op on a
+ * floating-point type -> MPI_ERR_OP */
+static int check_op(int dtype, int op)
+{
+    if (ftar_oracle_esize(dtype) == 0 || op < FTAR_SUM || op >= FTAR_NOPS) return FTAR_ERR_ARG;
+    if (op >= FTAR_LAND && (dtype == FTAR_FLOAT32 || dtype == FTAR_FLOAT64)) return FTAR_ERR_OP;
+    return FTAR_SUCCESS;
+}
 
 int ftar_oracle_reduce_local(int dtype, int op, const void *in, void *inout, size_t n)
 {
-    if (op < FTAR_SUM || op > FTAR_MIN) return FTAR_ERR_ARG;
+    int rc = check_op(dtype, op);
+    if (rc) return rc;
     switch (dtype) {
     case FTAR_INT32: reduce_i32(op, (const int32_t *)in, (int32_t *)inout, n); break;
     case FTAR_INT64: reduce_i64(op, (const int64_t *)in, (int64_t *)inout, n); break;
@@ -380,8 +418,8 @@ int ftar_oracle_rabenseifner(int p, size_t count, int dtype, int op, const void 
     memset(&S, 0, sizeof(S));
     S.p = p; S.count = count; S.dtype = dtype; S.op = op; S.kills = kills; S.nkills = nkills;
     S.res = res; S.es = ftar_oracle_esize(dtype);
-    if (p < 1 || p > FTAR_MAX_RANKS || S.es == 0 || op < FTAR_SUM || op > FTAR_MIN) {
-        res->ret = FTAR_ERR_ARG;
+    if (p < 1 || p > FTAR_MAX_RANKS || check_op(dtype, op)) {
+        res->ret = p < 1 || p > FTAR_MAX_RANKS ? FTAR_ERR_ARG : check_op(dtype, op);
         return res->ret;
     }
     size_t es = S.es;
@@ -735,8 +773,8 @@ int ftar_oracle_recursive_doubling(int p, size_t count, int dtype, int op, const
     memset(&S, 0, sizeof(S));
     S.p = p; S.count = count; S.dtype = dtype; S.op = op; S.kills = kills; S.nkills = nkills;
     S.res = res; S.es = ftar_oracle_esize(dtype);
-    if (p < 1 || p > FTAR_MAX_RANKS || S.es == 0 || op < FTAR_SUM || op > FTAR_MIN) {
-        res->ret = FTAR_ERR_ARG;
+    if (p < 1 || p > FTAR_MAX_RANKS || check_op(dtype, op)) {
+        res->ret = p < 1 || p > FTAR_MAX_RANKS ? FTAR_ERR_ARG : check_op(dtype, op);
         return res->ret;
     }
     size_t es = S.es;

@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(HERE, "_build", "libftar_oracle.so")
 
 INT32, FLOAT32, INT64, FLOAT64 = 0, 1, 2, 3
 SUM, PROD, MAX, MIN = 0, 1, 2, 3
+LAND, BAND, LOR, BOR, LXOR, BXOR = 4, 5, 6, 7, 8, 9  # MPI logical / bitwise ops (integer types)
 PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
 PT_BEFORE, PT_AFTER, PT_BARRIER, PT_DURING = 0, 1, 2, 3
 OK, DEAD, ABORTED = 0, 1, 2

@@ -176,19 +176,33 @@ int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, 
     return 1;
 }
 
-#define LOOP(T, UT)                                                                                         \
+/* one element op, the kernels' operand roles (ftar_kernels.hip apply): the arithmetic
+ * ops for every type, MPI's logical / bitwise ops (op >= 4) for the integer types only */
+#define DEF_OP(NAME, T, UT, INTEGER)                                                                        \
+    static inline T NAME(int op, T a, T b)                                                                  \
+    {                                                                                                       \
+        switch (op) {                                                                                       \
+        case 0: return (T)((UT)a + (UT)b);                                                                  \
+        case 1: return (T)((UT)a * (UT)b);                                                                  \
+        case 2: return (a > b) ? a : b;                                                                     \
+        case 3: return (a < b) ? a : b;                                                                     \
+        default: return INTEGER(op, a, b);                                                                  \
+        }                                                                                                   \
+    }
+#define INT_OPS(op, a, b)                                                                                   \
+    ((op) == 4 ? ((a) != 0 && (b) != 0) : (op) == 5 ? ((a) & (b)) : (op) == 6 ? ((a) != 0 || (b) != 0)       \
+     : (op) == 7 ? ((a) | (b)) : (op) == 8 ? (((a) != 0) != ((b) != 0)) : ((a) ^ (b)))
+#define NO_OPS(op, a, b) (a) /* never reached: the library refuses these ops on float types */
+DEF_OP(op_i32, int32_t, uint32_t, INT_OPS)
+DEF_OP(op_i64, int64_t, uint64_t, INT_OPS)
+DEF_OP(op_f32, float, float, NO_OPS)
+DEF_OP(op_f64, double, double, NO_OPS)
+
+#define LOOP(T, FN)                                                                                         \
     do {                                                                                                    \
         T *o = (T *)s->out;                                                                                 \
         const T *x = (const T *)s->x, *y = (const T *)s->y;                                                 \
-        for (size_t i = 0; i < s->n; i++) {                                                                 \
-            T a = x[i], b = y[i];                                                                           \
-            switch (op) {                                                                                   \
-            case 0: o[i] = (T)((UT)a + (UT)b); break;                                                       \
-            case 1: o[i] = (T)((UT)a * (UT)b); break;                                                       \
-            case 2: o[i] = (a > b) ? a : b; break;                                                          \
-            default: o[i] = (a < b) ? a : b; break;                                                         \
-            }                                                                                               \
-        }                                                                                                   \
+        for (size_t i = 0; i < s->n; i++) o[i] = FN(op, x[i], y[i]);                                        \
     } while (0)
 
 static size_t esz(int dt) { return (dt == 0 || dt == 1) ? 4 : 8; }
@@ -201,10 +215,10 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
             memmove(s->out, s->x, s->n * esz(dtype));
         } else {
             switch (dtype) {
-            case 0: LOOP(int32_t, uint32_t); break;
-            case 1: LOOP(float, float); break;
-            case 2: LOOP(int64_t, uint64_t); break;
-            default: LOOP(double, double); break;
+            case 0: LOOP(int32_t, op_i32); break;
+            case 1: LOOP(float, op_f32); break;
+            case 2: LOOP(int64_t, op_i64); break;
+            default: LOOP(double, op_f64); break;
             }
         }
         if (s->out2) memmove(s->out2, s->out, s->n * esz(dtype));
@@ -213,21 +227,13 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
     return 0;
 }
 
-#define TREE(T, UT)                                                                                         \
+#define TREE(T, FN)                                                                                         \
     do {                                                                                                    \
         for (size_t i = 0; i < n; i++) {                                                                    \
             T v[16];                                                                                        \
             for (int j = 0; j < nsrc; j++) v[j] = ((const T *)src[j])[i];                                   \
             for (int w = 1; w < nsrc; w <<= 1)                                                              \
-                for (int j = 0; j < nsrc; j += 2 * w) {                                                     \
-                    T a = v[j], b = v[j + w];                                                               \
-                    switch (op) {                                                                           \
-                    case 0: v[j] = (T)((UT)a + (UT)b); break;                                               \
-                    case 1: v[j] = (T)((UT)a * (UT)b); break;                                               \
-                    case 2: v[j] = (a > b) ? a : b; break;                                                  \
-                    default: v[j] = (a < b) ? a : b; break;                                                 \
-                    }                                                                                       \
-                }                                                                                           \
+                for (int j = 0; j < nsrc; j += 2 * w) v[j] = FN(op, v[j], v[j + w]);                        \
             ((T *)out)[i] = v[0];                                                                           \
         }                                                                                                   \
     } while (0)
@@ -237,10 +243,10 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
 {
     if (!(nsrc == 2 || nsrc == 4 || nsrc == 8 || nsrc == 16)) return 13;
     switch (dtype) {
-    case 0: TREE(int32_t, uint32_t); break;
-    case 1: TREE(float, float); break;
-    case 2: TREE(int64_t, uint64_t); break;
-    default: TREE(double, double); break;
+    case 0: TREE(int32_t, op_i32); break;
+    case 1: TREE(float, op_f32); break;
+    case 2: TREE(int64_t, op_i64); break;
+    default: TREE(double, op_f64); break;
     }
     d->ctr.link_bytes += (double)n * (double)esz(dtype) * __builtin_popcount(remote_mask);
     d->ctr.launches[tag]++;

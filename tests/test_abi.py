@@ -95,3 +95,23 @@ def test_oracle_is_not_linked_into_the_product(built):
     out = subprocess.run(["ldd", built], capture_output=True, text=True).stdout
     assert "oracle" not in out
     assert not any("oracle" in s for s in exported_symbols(built))
+
+
+def test_op_type_check_before_any_device_call(built):
+    """MPI_Reduce_local's type/op rule at the boundary, before anything touches a GPU:
+    a logical / bitwise op on a float type is MPI_ERR_OP (9), an unknown op or type is
+    MPI_ERR_ARG (13); every op MPI defines for the integer types is accepted (an empty
+    reduce returns success without a device)."""
+    L = ctypes.CDLL(built)
+    L.ftar_reduce_local.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p]
+    for dt in (0, 2):  # int32, int64
+        for op in range(10):
+            assert L.ftar_reduce_local(None, None, 0, dt, op, None) == 0, (dt, op)
+    for dt in (1, 3):  # float32, float64
+        for op in range(4):
+            assert L.ftar_reduce_local(None, None, 0, dt, op, None) == 0, (dt, op)
+        for op in range(4, 10):
+            assert L.ftar_reduce_local(None, None, 0, dt, op, None) == 9, (dt, op)
+    assert L.ftar_reduce_local(None, None, 0, 0, 10, None) == 13
+    assert L.ftar_reduce_local(None, None, 0, 4, 0, None) == 13

@@ -133,3 +133,34 @@ def test_reduce_local_rejects_bad_args(ftar):
     x = torch.zeros(16, device="cuda")
     with pytest.raises(ftar.FtarError):
         ftar.reduce_local(x, x, dtype=9)
+
+
+@pytest.mark.parametrize("dt", [0, 2])
+@pytest.mark.parametrize("op", [4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("n", [1, 17, 65537, 1 << 20])
+def test_reduce_local_logical_bitwise(ftar, oracle, dt, op, n):
+    """MPI's logical / bitwise ops on the integer types: vector body, heads and tails
+    bit-exact to the oracle; inputs carry zeros for the logical ops."""
+    import torch
+    a, b = _inputs(dt, n, seed=n * 3 + op)
+    a[::3] = 0
+    b[1::5] = 0
+    x, y = _to_dev(a), _to_dev(b)
+    ftar.reduce_local(x, y, op=op)
+    torch.cuda.synchronize()
+    want = b.copy()
+    oracle.reduce_local(a, want, op)
+    assert _same_bits(y.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("dt", [1, 3])
+def test_reduce_local_bitwise_on_float_refused(ftar, dt):
+    """MPI_ERR_OP before any launch; the output is untouched."""
+    import torch
+    x = torch.ones(1000, device="cuda", dtype=torch.float32 if dt == 1 else torch.float64)
+    y = torch.full_like(x, 2.0)
+    for op in range(4, 10):
+        with pytest.raises(ftar.FtarError, match="code 9"):
+            ftar.reduce_local(x, y, op=op)
+    torch.cuda.synchronize()
+    assert bool((y == 2.0).all())

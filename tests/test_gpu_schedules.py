@@ -426,3 +426,39 @@ def test_capped_grids_plain_stores(oracle, algo, p, env):
     _check(fn, algo, ins, op=2, env=dict(env, FTAR_BLOCKS_PER_CU="1", FTAR_NT_STORE="0"))
     _check(fn, algo, oracle.random_inputs(p, (1 << 20) + 37, seed=p * 13 + 6),
            env=dict(env, FTAR_BLOCKS_PER_CU="1"))
+
+
+def _bit_inputs(p, n, seed, dt):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(p):
+        v = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        v[rng.random(n) < 0.3] = 0
+        out.append(v)
+    return out
+
+
+@pytest.mark.parametrize("algo,p,op,count,env", [
+    ("raben", 8, 9, 100003, {"FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0"}),   # mesh (tree kernel)
+    ("raben", 8, 4, 4099, {}),                                                   # one-shot (tree batch)
+    ("raben", 4, 7, 65541, {"FTAR_MESH": "0"}),                                  # step by step
+    ("raben", 5, 6, 65541, {}),                                                  # pre/post-step + relay
+    ("raben", 2, 5, 100003, {}),
+    ("rd", 8, 8, 65541, {}),
+    ("rd", 6, 9, 4099, {"FTAR_RELAY": "0"}),
+    ("raben", 4, 9, 65541, {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0", "FTAR_MESH": "0"})])
+def test_schedule_logical_bitwise(oracle, algo, p, op, count, env):
+    """MPI's logical / bitwise ops (int32 / int64) through every kernel form the schedules
+    use -- tree, tree batch, segment, copy engine + local reduce -- bit-exact to the oracle."""
+    dt = np.int64 if op % 2 else np.int32
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    _check(fn, algo, _bit_inputs(p, count, p * 17 + op, dt), op=op, env=env)
+
+
+@pytest.mark.parametrize("algo,p,kill,op", [("raben", 9, (6, 1, 1, 3), 9), ("raben", 9, (6, 2, 1, 3), 4),
+                                            ("rd", 6, (3, 1, 1, 3), 7)])
+def test_kill_logical_bitwise(oracle, algo, p, kill, op):
+    """A kill mid-exchange under a bitwise op: recovery replays with the call's op."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    o, _ = _check(fn, algo, _bit_inputs(p, 65541, p + op, np.int32), [kill], op=op)
+    assert not o.aborted and o.recoveries >= 1

@@ -573,17 +573,23 @@ TRANSPORTS = [{}, {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}, {"FTAR_COPY_ENGINE"
 @settings(max_examples=int(os.environ.get("FTAR_PROPERTY_EXAMPLES", "120")), deadline=None,
           suppress_health_check=[HealthCheck.function_scoped_fixture])
 @given(algo=st.sampled_from(["raben", "rd"]), p=st.integers(1, 13), count=st.integers(1, 3000),
-       dtype=st.sampled_from([np.float32, np.int32, np.int64, np.float64]), op=st.integers(0, 3),
+       dtype=st.sampled_from([np.float32, np.int32, np.int64, np.float64]), op=st.integers(0, 9),
        transport=st.integers(0, len(TRANSPORTS) - 1), kill=st.none() | st.tuples(
            st.integers(0, 12), st.integers(0, 3), st.integers(0, 3), st.integers(0, 3)),
        seed=st.integers(0, 10 ** 6))
 def test_property_any_shape_transport_kill(hostsim, oracle, algo, p, count, dtype, op, transport, kill, seed):
     """Any rank count, ragged length, dtype, op, transport and (optionally) one kill point:
     the outcome class and every survivor's bits equal the oracle's (floats carry NaN /
-    signed zeros / infinities, so MAX / MIN pin the operand order)."""
+    signed zeros / infinities, so MAX / MIN pin the operand order; integers also take
+    MPI's logical / bitwise ops, on inputs with zeros)."""
+    if op >= 4 and dtype in (np.float32, np.float64):
+        op %= 4  # logical / bitwise ops exist for the integer types only (MPI_ERR_OP)
     ins = oracle.random_inputs(p, count, seed=seed, dtype=dtype)
     if dtype in (np.float32, np.float64):
         ins = H.with_specials(ins, p + 2)
+    elif op in (4, 6, 8):
+        for x in ins:
+            x[::3] = 0
     kills = []
     if kill is not None and kill[0] < p:
         kills = [kill]
@@ -636,3 +642,31 @@ def test_property_multi_kill_repeated_calls(hostsim, oracle, algo, p, count, dty
         for it in range(1, iters):
             i = o1.order_after.index(w)
             assert np.array_equal(r.outputs[w][it].view(u), o2.outputs[i].view(u)), (ks, w, it)
+
+
+def _bit_inputs(p, n, seed, dt):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(p):
+        v = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        v[rng.random(n) < 0.3] = 0
+        out.append(v)
+    return out
+
+
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p,op", [(3, 4), (4, 5), (5, 6), (8, 7), (9, 8), (6, 9), (2, 9), (16, 5)])
+def test_nofault_logical_bitwise(hostsim, oracle, algo, p, op):
+    """MPI's logical / bitwise ops (integer types) through both schedules, every
+    transport's code path the defaults pick (mesh / one-shot at powers of two)."""
+    dt = np.int64 if p % 2 else np.int32
+    _cmp(_fn(oracle, algo), algo, _bit_inputs(p, 1031, p * 13 + op, dt), op=op)
+
+
+@pytest.mark.parametrize("algo,p,kill", [("raben", 9, (6, 1, 1, 3)), ("raben", 5, (4, 2, 0, 0)), ("rd", 6, (3, 1, 1, 3)),
+                                         ("rd", 8, (5, 1, 0, 1))])
+@pytest.mark.parametrize("op", [4, 7, 9])
+def test_kill_logical_bitwise(hostsim, oracle, algo, p, kill, op):
+    """A recovering kill under a bitwise op: the handlers' replays and re-sends reduce
+    with the call's op (not SUM)."""
+    _cmp(_fn(oracle, algo), algo, _bit_inputs(p, 777, p + op, np.int32), [kill], op=op)

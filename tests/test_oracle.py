@@ -203,3 +203,58 @@ def test_reference_wrong_result_rows_are_harness_artefacts(oracle):
         for n in sorted({r["N"] for r in wrong}):
             o = fn(oracle.rank_inputs(n, 257))
             assert all(oracle.checksum17(x) == oracle.expected_checksum(n, 257) for x in o.outputs), (algo, n)
+
+
+# MPI's logical and bitwise predefined ops (include/ftar.h): numpy restatements
+BIT_OPS = {4: lambda b, a: ((b != 0) & (a != 0)), 5: lambda b, a: b & a, 6: lambda b, a: ((b != 0) | (a != 0)),
+           7: lambda b, a: b | a, 8: lambda b, a: ((b != 0) ^ (a != 0)), 9: lambda b, a: b ^ a}
+
+
+def bit_inputs(p, n, seed, dt):
+    """Integers with many zeros (the logical ops) and full-width bit patterns (the bitwise ones)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for r in range(p):
+        v = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        v[rng.random(n) < 0.3] = 0
+        out.append(v)
+    return out
+
+
+@pytest.mark.parametrize("dt", [np.int32, np.int64])
+@pytest.mark.parametrize("op", [4, 5, 6, 7, 8, 9])
+def test_reduce_local_logical_bitwise(oracle, dt, op):
+    a, b = bit_inputs(2, 4099, op, dt)
+    inout = b.copy()
+    oracle.reduce_local(a, inout, op)
+    assert (inout == BIT_OPS[op](b, a).astype(dt)).all()
+
+
+@pytest.mark.parametrize("op", [4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_logical_bitwise_on_float_is_err_op(oracle, op, dt):
+    """MPI_ERR_OP (9) for a logical / bitwise op on a floating-point type, in the local
+    reduce and in both schedules; unknown ops are MPI_ERR_ARG."""
+    a = np.ones(8, dt)
+    b = np.ones(8, dt)
+    rc = oracle.lib().ftar_oracle_reduce_local(oracle.DTYPE_OF[a.dtype], op, a.ctypes.data, b.ctypes.data, 8)
+    assert rc == 9
+    assert oracle.rabenseifner([a, b], op=op).ret == 9
+    assert oracle.recursive_doubling([a, b], op=op).ret == 9
+    assert oracle.rabenseifner([a, b], op=10).ret == 13
+
+
+@pytest.mark.parametrize("algo", ["rd", "raben"])
+@pytest.mark.parametrize("p", [2, 3, 5, 8, 9])
+@pytest.mark.parametrize("op", [4, 5, 6, 7, 8, 9])
+def test_schedules_logical_bitwise(oracle, algo, p, op):
+    """Every rank ends with the fold of all inputs (these ops commute and associate
+    exactly, so any schedule order gives the numpy fold)."""
+    from functools import reduce
+    dt = np.int64 if op % 2 else np.int32
+    ins = bit_inputs(p, 1031, p * 10 + op, dt)
+    want = reduce(lambda acc, x: BIT_OPS[op](acc, x).astype(dt), ins[1:], ins[0])
+    r = (oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling)(ins, op=op)
+    assert r.ret == 0
+    for w in range(p):
+        assert (r.outputs[w] == want).all(), w
