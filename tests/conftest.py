@@ -66,3 +66,15 @@ def hostsim():
 @pytest.fixture(scope="session")
 def ftar():
     return load_package()
+
+
+# Tests that drive the GPU from the pytest process itself (torch tensors in-process) go
+# last: once this process holds a GPU context, every multi-rank job after it has one
+# process more on the device than it launches, and at 8 ranks that exceeds the 8
+# process slots (VMIDs) the hardware scheduler runs at once -- the job's processes are
+# then time-sliced and an 8-rank case takes 2-4x longer.
+IN_PROCESS_GPU = ("test_gpu_kernels.py",)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=lambda it: os.path.basename(str(it.fspath)) in IN_PROCESS_GPU)
