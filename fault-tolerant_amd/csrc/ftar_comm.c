@@ -576,20 +576,26 @@ void *ftar_local(ftar_comm *c, int b)
     return ftar_buf(c, c->wrank, b);
 }
 
+/* Grow the exported workspace.  The new blocks are allocated, exported and imported
+ * while the old ones -- ours and our imports of the peers' -- are still mapped, and only
+ * then are the old mappings closed and the old blocks freed.  The other order (close,
+ * free, allocate, export) let a fresh hipMalloc land on the address range an import had
+ * occupied a moment before, and the runtime then refused to export it
+ * (hipIpcGetMemHandle: invalid argument; seen once in 8-rank regrowth sweeps, round 1 and
+ * round 2).  Costs the old workspace's memory for the length of the call. */
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
 {
     if (bytes <= c->ws_bytes && c->ws[0]) return FTAR_SUCCESS;
     if (c->ws[0] && bytes < 2 * c->ws_bytes) bytes = 2 * c->ws_bytes; /* grow geometrically: few re-exports */
     size_t nb = (bytes + WS_ALIGN - 1) / WS_ALIGN * WS_ALIGN;
     if (nb == 0) nb = WS_ALIGN;
-    ftar_sync_fatal(c); /* everybody is here */
-    release_peers(c);
-    ftar_sync_fatal(c); /* nobody maps the old buffers */
+    void *old_ws[FTAR_NBUF];
+    void *old_peer[FTAR_MAX_RANKS][FTAR_NBUF];
+    memcpy(old_ws, c->ws, sizeof(old_ws));
+    memcpy(old_peer, c->peer, sizeof(old_peer));
+    memset(c->peer, 0, sizeof(c->peer));
+    ftar_sync_fatal(c); /* everybody is here: nobody reads a workspace until this returns */
     ftar_slot *me = &c->job.shm->slot[c->wrank];
-    for (int b = 0; b < FTAR_NBUF; b++) {
-        fdev_free(c->dev, c->ws[b]);
-        c->ws[b] = NULL;
-    }
     for (int b = 0; b < FTAR_NBUF; b++) {
         int rc = fdev_alloc_shared(c->dev, nb, &c->ws[b], me->handle[b]);
         if (rc) {
@@ -601,7 +607,7 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
     me->ws_bytes = nb;
     atomic_fetch_add(&me->ws_gen, 1);
     c->ws_bytes = nb;
-    ftar_sync_fatal(c); /* every handle is published */
+    ftar_sync_fatal(c); /* every new handle is published */
     for (int i = 0; i < c->size; i++) {
         int w = c->order[i];
         if (w == c->wrank) continue;
@@ -616,6 +622,11 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
         }
         c->peer_bytes[w] = s->ws_bytes;
     }
+    for (int w = 0; w < c->wsize; w++) /* the old mappings, dead ranks' included */
+        for (int b = 0; b < FTAR_NBUF; b++)
+            if (old_peer[w][b]) fdev_unimport(c->dev, old_peer[w][b]);
+    ftar_sync_fatal(c); /* nobody maps the old buffers */
+    for (int b = 0; b < FTAR_NBUF; b++) fdev_free(c->dev, old_ws[b]);
     return FTAR_SUCCESS;
 }
 

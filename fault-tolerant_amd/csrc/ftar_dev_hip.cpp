@@ -173,13 +173,15 @@ void fdev_close(ftar_dev *d)
 int fdev_device(const ftar_dev *d) { return d->device; }
 
 // Round 1 saw one refused export (hipIpcGetMemHandle: invalid argument) when a sweep
-// re-allocated the workspace at every size.  tools/ipc_probe.hip (profiles/r02) found no
-// refusal in the library's growth pattern -- 10 rounds of 4 blocks x 2 ranks, imports
-// closed before the free, closed-import VA ranges checked for reuse -- and the workspace
-// now grows geometrically, so a job re-allocates O(log S) times.  A refusal is still
-// handled, bounded and visible: the refused block is held while ONE more is tried (so the
-// retry lands at another address), the event is printed and counted
-// (ftar_stats.export_retries; tests assert it stays 0).
+// re-allocated the workspace at every size, and round 2's 8-rank regrowth test saw it
+// once more, on a fresh 18 MiB block.  tools/ipc_probe.hip found no refusal in isolation;
+// the pattern both failures share is an allocation made right after this process closed
+// its imports of the peers' old blocks (ftar_ensure_workspace closed, freed, then
+// allocated), so the fresh block could land on an address range an import had just
+// released.  ftar_ensure_workspace now allocates and exports the new blocks while every
+// old mapping is still in place.  A refusal is still handled, bounded and visible: the
+// refused block is held while ONE more is tried (so the retry lands at another address),
+// the event is printed and counted (ftar_stats.export_retries; tests assert it stays 0).
 int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
 {
     HIPCHK(hipSetDevice(d->device));
