@@ -111,10 +111,12 @@ def _dtype_of(t) -> int:
 
 
 def _ptr(x):
+    """A buffer of the device entry points: a contiguous tensor on the comm's GPU, or a
+    pinned host tensor (the kernels read and write it in place over PCIe; include/ftar.h)."""
     if isinstance(x, int):
         return x
-    if not x.is_cuda or not x.is_contiguous():
-        raise FtarError("buffers must be contiguous device tensors")
+    if not x.is_contiguous() or not (x.is_cuda or x.is_pinned()):
+        raise FtarError("buffers must be contiguous device tensors or pinned host tensors")
     return x.data_ptr()
 
 
@@ -125,15 +127,18 @@ def _check(rc: int, what: str):
 
 def reduce_local(inp, inout, count=None, dtype=None, op: int = SUM, stream=None):
     """MPI_Reduce_local(in, inout): inout = inout <op> in on the GPU (asynchronous on
-    `stream`, default the current torch stream)."""
+    `stream`, default the current torch stream).  Operands may be pinned host tensors
+    (zero copy over PCIe)."""
     if count is None:
         count = inout.numel()
     if dtype is None:
         dtype = _dtype_of(inout)
     if stream is None and not isinstance(inout, int):
         import torch
-        stream = torch.cuda.current_stream(inout.device).cuda_stream
-    _check(lib().ftar_reduce_local(_ptr(inp), _ptr(inout), count, dtype, op, stream or None), "ftar_reduce_local")
+        dev = inout.device if inout.is_cuda else (inp.device if getattr(inp, "is_cuda", False) else None)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    _check(lib().ftar_reduce_local(_ptr(inp), _ptr(inout), count, dtype, op, stream or None),
+           "ftar_reduce_local")
 
 
 def set_reduce_variant(v: int):

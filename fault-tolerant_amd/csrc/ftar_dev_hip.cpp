@@ -242,6 +242,14 @@ int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, 
     unsigned long long bid = 0;
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    // only this device's HBM is exported; pinned host memory (which the kernels may read
+    // and write in place) is staged instead
+    if (hipPointerGetAttributes(&a, ptr) != hipSuccess || a.type != hipMemoryTypeDevice || a.device != d->device) {
+        (void)hipGetLastError();
+        return 1;
+    }
     if (hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)ptr) != hipSuccess || bid == 0 ||
         hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
         (void)hipGetLastError();
@@ -685,6 +693,30 @@ int fdev_set_reduce_variant(int v)
     return 0;
 }
 
+// An operand of the local reduce: memory of device `dev` (the whole range inside one
+// allocation) or pinned host memory, which the kernel reads and writes in place over PCIe
+// (zero copy: the reads use the link's host-to-device direction while the stores use the
+// other).  Pageable or unknown memory is refused before any launch: a kernel touching it
+// would fault the GPU.
+static int check_local_ptr(const void *ptr, size_t bytes, int dev)
+{
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    if (hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    if (a.type == hipMemoryTypeHost) return 0;
+    if (a.type != hipMemoryTypeDevice || a.device != dev) return 1;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    return (size_t)((const char *)ptr - (const char *)base) + bytes > size;
+}
+
 int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream)
 {
     size_t es = esize_of(dtype);
@@ -695,6 +727,10 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
     if (n == 0) return 0;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
+    if (n > SIZE_MAX / es || check_local_ptr(in, n * es, dev) || check_local_ptr(inout, n * es, dev)) {
+        snprintf(g_err, sizeof(g_err), "reduce_local: operands must be memory of device %d or pinned host memory", dev);
+        return 13;
+    }
     hipDeviceProp_t prop;
     static int cached_dev = -1;
     static unsigned cached_blocks = 2048;

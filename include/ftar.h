@@ -168,7 +168,12 @@ int ftar_recursive_doubling_host(const void *src, void *dst, size_t count,
 
 /* MPI_Reduce_local(in, inout, count, dtype, op) on the device:
  * inout[i] = in[i] (op) inout[i] with the reference's operand roles.
- * `stream` is a hipStream_t (NULL = null stream); the call is asynchronous. */
+ * `stream` is a hipStream_t (NULL = null stream); the call is asynchronous.
+ * Each operand is memory of the current device or pinned host memory (hipHostMalloc /
+ * hipHostRegister): the reference reduces host buffers, and on pinned ones the kernel
+ * reads and writes them in place over PCIe (zero copy, both link directions at once).
+ * Pageable or unknown memory, or a range past its allocation: FTAR_ERR_ARG, nothing
+ * launched. */
 int ftar_reduce_local(const void *in, void *inout, size_t count,
                       ftar_dtype dtype, ftar_op op, void *stream);
 

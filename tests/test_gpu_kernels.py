@@ -164,3 +164,99 @@ def test_reduce_local_bitwise_on_float_refused(ftar, dt):
             ftar.reduce_local(x, y, op=op)
     torch.cuda.synchronize()
     assert bool((y == 2.0).all())
+
+
+def _pinned(a):
+    import torch
+    return torch.from_numpy(a.copy()).pin_memory()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("dt", [0, 1, 2, 3])
+@pytest.mark.parametrize("op", [0, 2, 3])
+@pytest.mark.parametrize("n", [1, 17, 65537, (1 << 20) + 256])
+def test_reduce_local_pinned_host(ftar, oracle, variant, dt, op, n):
+    """The reference's MPI_Reduce_local works on host buffers: with pinned ones the kernel
+    reads and writes them in place over PCIe (zero copy).  Bit-exact to the oracle, both
+    kernels, the vector body and the scalar heads / tails."""
+    import torch
+    a, b = _inputs(dt, n, seed=n * 5 + op + dt, specials=op >= 2)
+    x, y = _pinned(a), _pinned(b)
+    ftar.set_reduce_variant(variant)
+    try:
+        ftar.reduce_local(x, y, op=op)
+        torch.cuda.synchronize()
+    finally:
+        ftar.set_reduce_variant(0)
+    want = b.copy()
+    oracle.reduce_local(a, want, op)
+    assert _same_bits(y.numpy(), want)
+
+
+@pytest.mark.parametrize("where", ["in_host", "inout_host"])
+def test_reduce_local_mixed_host_device(ftar, oracle, where):
+    """One operand in pinned host memory, the other in HBM."""
+    import torch
+    n = 300007
+    a, b = _inputs(1, n, seed=23)
+    x = _pinned(a) if where == "in_host" else _to_dev(a)
+    y = _pinned(b) if where == "inout_host" else _to_dev(b)
+    ftar.reduce_local(x, y, op=0)
+    torch.cuda.synchronize()
+    want = b.copy()
+    oracle.reduce_local(a, want, 0)
+    assert _same_bits(y.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("off_in,off_io", [(1, 1), (1, 2)])
+def test_reduce_local_pinned_unaligned(ftar, oracle, off_in, off_io):
+    import torch
+    n = 100003
+    a, b = _inputs(1, n + 8, seed=29)
+    x, y = _pinned(a), _pinned(b)
+    ftar.reduce_local(x[off_in:off_in + n], y[off_io:off_io + n], count=n, dtype=1, op=0)
+    torch.cuda.synchronize()
+    want = b.copy()
+    part = want[off_io:off_io + n].copy()
+    oracle.reduce_local(a[off_in:off_in + n].copy(), part, 0)
+    want[off_io:off_io + n] = part
+    assert _same_bits(y.numpy(), want)
+
+
+def test_reduce_local_c2_pinned_host_full_size(ftar):
+    """C2's two 256 MiB float32 vectors in pinned host memory, reduced in place over PCIe
+    (bench.py's e2e.zero_copy); checked against torch's fp32 add on the CPU (one IEEE add
+    per element, so bit-identical)."""
+    import torch
+    n = 1 << 26
+    g = torch.Generator().manual_seed(13)
+    x = (torch.rand(n, generator=g) * 2 - 1).pin_memory()
+    y = (torch.rand(n, generator=g) * 2 - 1).pin_memory()
+    want = y + x
+    ftar.set_reduce_variant(1)
+    try:
+        ftar.reduce_local(x, y, op=0)
+        torch.cuda.synchronize()
+    finally:
+        ftar.set_reduce_variant(0)
+    assert torch.equal(y.view(torch.int32), want.view(torch.int32))
+
+
+def test_reduce_local_refuses_pageable_and_overruns(ftar):
+    """Pageable host memory (a kernel touching it would fault the GPU) and a range past
+    its device allocation are refused with FTAR_ERR_ARG before any launch."""
+    import torch
+    page = np.arange(4096, dtype=np.float32)
+    y = torch.full((4096,), 2.0, device="cuda")
+    with pytest.raises(ftar.FtarError, match="code 13"):
+        ftar.reduce_local(page.ctypes.data, y, count=4096, dtype=1)
+    with pytest.raises(ftar.FtarError, match="code 13"):
+        ftar.reduce_local(y, page.ctypes.data, count=4096, dtype=1)
+    with pytest.raises(ftar.FtarError):
+        ftar.reduce_local(torch.from_numpy(page), y)  # not pinned: refused in the binding
+    x = torch.ones(16, device="cuda")
+    with pytest.raises(ftar.FtarError, match="code 13"):
+        ftar.reduce_local(x, y, count=1 << 30, dtype=1)
+    torch.cuda.synchronize()
+    assert bool((y == 2.0).all())
+    assert np.array_equal(page, np.arange(4096, dtype=np.float32))

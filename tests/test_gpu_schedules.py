@@ -462,3 +462,23 @@ def test_kill_logical_bitwise(oracle, algo, p, kill, op):
     fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
     o, _ = _check(fn, algo, _bit_inputs(p, 65541, p + op, np.int32), [kill], op=op)
     assert not o.aborted and o.recoveries >= 1
+
+
+@pytest.mark.parametrize("algo,p,mode", [("raben", 2, {}), ("raben", 4, {}), ("raben", 4, {"FTAR_ONESHOT_MAX": "0"}),
+                                         ("raben", 8, {"FTAR_PROBE_INPLACE": "1", "FTAR_ONESHOT_MAX": "0"}),
+                                         ("raben", 5, {}), ("raben", 4, {"FTAR_MESH": "0", "FTAR_PROBE_OFFSET": "1"}),
+                                         ("rd", 4, {}), ("rd", 6, {"FTAR_PROBE_INPLACE": "1"})])
+def test_pinned_host_buffers(oracle, algo, p, mode):
+    """The device entry points on pinned host buffers: this rank's kernels read sbuf and
+    write rbuf in place over PCIe (zero copy), peers read the staged copy in HBM (host
+    memory is never exported).  One-shot, mesh, spare, step-by-step and RD forms; in
+    place and at element offsets; two calls; sbuf untouched; bit-exact to the oracle."""
+    ins = oracle.random_inputs(p, 65536 + 17, seed=p + 190)
+    o = (oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling)(ins)
+    r = H.run_torch_worker(algo, ins, devmap=ALL_ON_GPU0, env_extra=dict(mode, FTAR_PROBE_PINNED="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    for w in range(p):
+        assert len(r.outputs.get(w, [])) == 2, r.stderr[-2000:]
+        for it in range(2):
+            assert r.status[w][it] == (0, 1), (w, it, r.status[w][it])
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)

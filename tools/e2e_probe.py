@@ -1,6 +1,8 @@
 """End-to-end (host buffers) Raben timing under ftrun: pinned H2D + device Allreduce +
 D2H per call, the chunk pipeline on and off (FTAR_HOST_PIPE is read per job, so this
-runs the job twice via the caller).
+runs the job twice via the caller).  E2E_ZERO_COPY=1 times the device entry point on the
+same pinned buffers instead: this rank's kernels read sbuf and write rbuf over PCIe, only
+the part peers pull is staged in HBM.
 
     fault-tolerant_amd/bin/ftrun -np 2 --devmap 0,0 python tools/e2e_probe.py [count]
 """
@@ -26,18 +28,21 @@ def main():
     comm.set_profiling(os.environ.get("FTAR_PROFILE", "0") == "1")
     xh = (torch.rand(n) * 2 - 1).pin_memory()
     yh = torch.empty_like(xh).pin_memory()
+    zc = os.environ.get("E2E_ZERO_COPY", "0") == "1"
+    fn = comm.allreduce_rabenseifner if zc else comm.allreduce_rabenseifner_host
     for _ in range(2):
-        assert comm.allreduce_rabenseifner_host(xh, yh) == 0
+        assert fn(xh, yh) == 0
     ts = []
     for _ in range(5):
         comm.barrier()
         t0 = time.perf_counter()
-        assert comm.allreduce_rabenseifner_host(xh, yh) == 0
+        assert fn(xh, yh) == 0
+        torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     ts.sort()
     if rank == 0:
         print(json.dumps({"ranks": int(os.environ["FTAR_SIZE"]), "count": n,
-                          "host_pipe": os.environ.get("FTAR_HOST_PIPE", "1"),
+                          "host_pipe": os.environ.get("FTAR_HOST_PIPE", "1"), "zero_copy": zc,
                           "profiling": os.environ.get("FTAR_PROFILE", "0"),
                           "ms_median": round(ts[len(ts) // 2] * 1e3, 3), "ms_min": round(ts[0] * 1e3, 3)}), flush=True)
     comm.finalize()

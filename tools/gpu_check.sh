@@ -15,7 +15,7 @@
 #   meshprof   rank 0 of a 4 / 8-rank mesh job under rocprofv3 (trace, FETCH_SIZE, WRITE_SIZE)
 #   campaign   tools/fault_campaign.sh: the reference's random-kill campaign, both schedules
 #   sweep      tools/size_sweep.py with 2 / 4 / 8 ranks on GPU 0
-#   e2e        host-buffer Raben end to end, chunk pipeline on / off
+#   e2e        host-buffer Raben end to end: chunk pipeline on / off, zero copy (1 / 2 / 4 ranks)
 #   syncprobe  tools/sync_probe.hip: device round trip of one step
 #   cpubase    tools/cpu_schedule_bench.py on this box's host cores
 #   xgmi       tools/xgmi_probe.hip: one link / all peers, pull / push / copy engines (loopback on one GPU)
@@ -102,11 +102,13 @@ if has sweep; then
   done
 fi
 if has e2e; then
-  # host-buffer Raben end to end, chunk pipeline on / off, 2 / 4 ranks on GPU 0
-  for n in 2 4; do for hp in 1 0; do
-    FTAR_HOST_PIPE=$hp timeout -k 10 200 fault-tolerant_amd/bin/ftrun -np $n --devmap 0,0,0,0 python -u tools/e2e_probe.py \
-        >> "$OUT/e2e.json" 2>> "$OUT/e2e.err"
-    rc=$?; stop_on_fault $rc e2e_${n}_$hp
+  # host-buffer Raben end to end, chunk pipeline on / off, and the device entry point on
+  # the same pinned buffers (zero copy), 1 / 2 / 4 ranks on GPU 0
+  for n in 1 2 4; do for mode in pipe1 pipe0 zc; do
+    hp=1; zc=0; [ $mode = pipe0 ] && hp=0; [ $mode = zc ] && zc=1
+    FTAR_HOST_PIPE=$hp E2E_ZERO_COPY=$zc timeout -k 10 200 fault-tolerant_amd/bin/ftrun -np $n --devmap 0,0,0,0 \
+        python -u tools/e2e_probe.py >> "$OUT/e2e.json" 2>> "$OUT/e2e.err"
+    rc=$?; stop_on_fault $rc e2e_${n}_$mode
   done; done
   cat "$OUT/e2e.json"
 fi
