@@ -237,6 +237,14 @@ class Comm:
             dtype = _dtype_of(dst)
         return lib().ftar_recursive_doubling(_ptr(src), _ptr(dst), count, dtype, op, self._h)
 
+    def recursive_doubling_host(self, src, dst, count=None, dtype=None, op: int = SUM) -> int:
+        """Host buffers (ideally pinned torch CPU tensors)."""
+        if count is None:
+            count = dst.numel()
+        if dtype is None:
+            dtype = _dtype_of(dst)
+        return lib().ftar_recursive_doubling_host(src.data_ptr(), dst.data_ptr(), count, dtype, op, self._h)
+
     def finalize(self):
         if self._h:
             _check(lib().ftar_finalize(self._h), "ftar_finalize")

@@ -78,6 +78,8 @@ int fdev_unimport(ftar_dev *d, void *ptr);
  * or pinned / managed memory; nonzero for pageable host memory or a range past the end
  * of its allocation (the device entry points refuse those instead of faulting). */
 int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes);
+/* 1 if `ptr` is pinned host memory (the kernels read and write it in place over PCIe) */
+int fdev_host_pinned(const void *ptr);
 
 /* Enqueue one segment kernel on the rank's stream. */
 int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);

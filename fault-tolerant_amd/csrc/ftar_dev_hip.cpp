@@ -72,6 +72,15 @@ struct Pending {
     int tag;
 };
 
+// Host memory a kernel may read and write through the caller's own pointer: pinned
+// (hipHostMalloc, or registered) AND mapped into the device at the same virtual address.
+// Registered memory can be mapped elsewhere (its device pointer then differs), and a
+// kernel using the host address would fault: such memory is treated as not shareable.
+bool host_same_va(const hipPointerAttribute_t &a)
+{
+    return a.type == hipMemoryTypeHost && a.hostPointer && a.hostPointer == a.devicePointer;
+}
+
 } // namespace
 
 struct ftar_dev {
@@ -288,6 +297,7 @@ int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes)
         return 1; // not memory the runtime knows (pageable host memory)
     }
     if (a.type == hipMemoryTypeUnregistered) return 1;
+    if (a.type == hipMemoryTypeHost) return !host_same_va(a);
     if (a.type == hipMemoryTypeDevice) {
         if (a.device != d->device) return 1; // another GPU's memory: the kernels run on ours
         hipDeviceptr_t base = nullptr;     // the whole range inside one allocation
@@ -299,6 +309,17 @@ int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes)
         if ((size_t)((const char *)ptr - (const char *)base) + bytes > size) return 1;
     }
     return 0;
+}
+
+int fdev_host_pinned(const void *ptr)
+{
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof(a));
+    if (!ptr || hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return host_same_va(a);
 }
 
 int fdev_unimport(ftar_dev *d, void *ptr)
@@ -706,7 +727,7 @@ static int check_local_ptr(const void *ptr, size_t bytes, int dev)
         (void)hipGetLastError();
         return 1;
     }
-    if (a.type == hipMemoryTypeHost) return 0;
+    if (a.type == hipMemoryTypeHost) return !host_same_va(a);
     if (a.type != hipMemoryTypeDevice || a.device != dev) return 1;
     hipDeviceptr_t base = nullptr;
     size_t size = 0;

@@ -683,7 +683,6 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
     if (orc) return orc;
     size_t es = ftar_esize(dtype);
     size_t bytes = count * es;
-    ftar_ensure_staging(c, bytes);
     /* Power of two without a spare (every failure aborts, so nothing is recovered across
      * calls): the vector goes through as a pipeline of chunk Allreduces -- chunk k's
      * H2D, chunk k-1's Allreduce and chunk k-2's D2H in flight at once (copy engines both
@@ -701,6 +700,11 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
         nchunk = (int)(bytes / HOST_PIPE_CHUNK);
         if (nchunk > HOST_PIPE_MAX) nchunk = HOST_PIPE_MAX;
     }
+    /* Not pipelined and the caller's buffers pinned: the device entry point reads sbuf and
+     * writes rbuf in place over PCIe, no staging copies */
+    if (nchunk <= 1 && fdev_host_pinned(sbuf) && fdev_host_pinned(rbuf))
+        return ftar_allreduce_rabenseifner(sbuf, rbuf, count, dtype, op, c);
+    ftar_ensure_staging(c, bytes);
     if (nchunk <= 1) {
         if (bytes && fdev_h2d(c->dev, c->hsend, sbuf, bytes)) return FTAR_ERR_DEVICE;
         int rc = ftar_allreduce_rabenseifner(c->hsend, c->hrecv, count, dtype, op, c);

@@ -310,6 +310,9 @@ int ftar_recursive_doubling_host(const void *src, void *dst, size_t count, ftar_
     if (orc) return orc;
     size_t es = ftar_esize(dtype);
     size_t bytes = count * es;
+    /* pinned caller buffers: the device entry point reads src and writes dst in place over
+     * PCIe (the last step's result goes straight to dst), no staging copies */
+    if (fdev_host_pinned(src) && fdev_host_pinned(dst)) return ftar_recursive_doubling(src, dst, count, dtype, op, c);
     ftar_ensure_staging(c, bytes);
     if (bytes && fdev_h2d(c->dev, c->hsend, src, bytes)) return FTAR_ERR_DEVICE;
     int rc = ftar_recursive_doubling(c->hsend, c->hrecv, count, dtype, op, c);

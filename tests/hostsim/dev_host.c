@@ -254,6 +254,7 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
 }
 
 int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes) { return ptr == NULL; }
+int fdev_host_pinned(const void *ptr) { return 0; } /* host-sim: the _host entry points always stage */
 
 int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
                     void *const *out, const size_t *n, int ntree, int tag)

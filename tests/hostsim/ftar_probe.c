@@ -12,8 +12,11 @@
  *      FTAR_PROBE_DEVICE=1 (device-pointer entry points on this process's own malloc buffers:
  *      host-sim: "device" memory is host memory; GPU build: must be refused),
  *      FTAR_PROBE_INPLACE=1 (send buffer = receive buffer),
- *      FTAR_PROBE_OFFSET=k (buffers start k elements past a 16-byte boundary)
+ *      FTAR_PROBE_OFFSET=k (buffers start k elements past a 16-byte boundary),
+ *      FTAR_PROBE_PINNED=1 (buffers from hipHostMalloc, looked up in the loaded HIP runtime:
+ *      the _host entry points then run zero copy; host-sim build: no runtime, plain memory)
  */
+#include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -21,6 +24,28 @@
 #include "ftar.h"
 
 static size_t esize(int dt) { return (dt == 0 || dt == 1) ? 4 : 8; }
+
+static char *probe_alloc(size_t n, int pinned)
+{
+    if (pinned) {
+        int (*host_malloc)(void **, size_t, unsigned) =
+            (int (*)(void **, size_t, unsigned))dlsym(RTLD_DEFAULT, "hipHostMalloc");
+        if (host_malloc) {
+            void *p = NULL;
+            return host_malloc(&p, n, 0) == 0 ? p : NULL;
+        }
+    }
+    return aligned_alloc(64, n);
+}
+
+static void probe_free(char *p, int pinned)
+{
+    int (*host_free)(void *) = pinned ? (int (*)(void *))dlsym(RTLD_DEFAULT, "hipHostFree") : NULL;
+    if (host_free)
+        host_free(p);
+    else
+        free(p);
+}
 
 int main(void)
 {
@@ -41,7 +66,10 @@ int main(void)
     ftar_world_rank(comm, &rank);
     size_t bytes = count * esize(dt);
     size_t pad = off * esize(dt);
-    char *in_mem = aligned_alloc(64, (bytes + pad + 64) / 64 * 64), *out_mem = aligned_alloc(64, (bytes + pad + 64) / 64 * 64);
+    int pinned = getenv("FTAR_PROBE_PINNED") ? atoi(getenv("FTAR_PROBE_PINNED")) : 0;
+    char *in_mem = probe_alloc((bytes + pad + 64) / 64 * 64, pinned);
+    char *out_mem = probe_alloc((bytes + pad + 64) / 64 * 64, pinned);
+    if (!in_mem || !out_mem) return 5;
     void *in = in_mem + pad, *out = out_mem + pad;
     char path[512];
     snprintf(path, sizeof(path), "%s/in_%d.bin", dir, rank);
@@ -83,7 +111,7 @@ int main(void)
     }
     ftar_finalize(comm);
     free(pristine);
-    free(in_mem);
-    free(out_mem);
+    probe_free(in_mem, pinned);
+    probe_free(out_mem, pinned);
     return 0;
 }

@@ -482,3 +482,17 @@ def test_pinned_host_buffers(oracle, algo, p, mode):
         for it in range(2):
             assert r.status[w][it] == (0, 1), (w, it, r.status[w][it])
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+
+
+@pytest.mark.parametrize("algo,p,kills,env", [
+    ("rd", 4, [], {}), ("rd", 6, [(3, 1, 1, 3)], {}), ("rd", 8, [(5, 1, 1, 2)], {"FTAR_PROBE_OFFSET": "1"}),
+    ("raben", 5, [], {}), ("raben", 9, [(6, 1, 1, 3)], {}), ("raben", 5, [(3, 2, 0, 1)], {"FTAR_PROBE_INPLACE": "1"}),
+    ("raben", 4, [], {"FTAR_HOST_PIPE": "0"}), ("raben", 4, [], {})])
+def test_host_entry_pinned_zero_copy(oracle, algo, p, kills, env):
+    """The _host entry points on pinned caller buffers (hipHostMalloc): where the call is
+    not chunk-pipelined they run the device entry point on the caller's buffers in place
+    (zero copy over PCIe, no staging), including kills mid-exchange and recoveries;
+    bit-exact to the oracle, sbuf untouched."""
+    ins = oracle.random_inputs(p, 65536 + 9, seed=p * 13 + len(kills))
+    _check(oracle.recursive_doubling if algo == "rd" else oracle.rabenseifner, algo, ins, kills,
+           env=dict(env, FTAR_PROBE_PINNED="1"))

@@ -1,6 +1,6 @@
 """End-to-end (host buffers) Raben timing under ftrun: pinned H2D + device Allreduce +
 D2H per call, the chunk pipeline on and off (FTAR_HOST_PIPE is read per job, so this
-runs the job twice via the caller).  E2E_ZERO_COPY=1 times the device entry point on the
+runs the job twice via the caller).  E2E_ALGO=rd times recursive doubling.  E2E_ZERO_COPY=1 times the device entry point on the
 same pinned buffers instead: this rank's kernels read sbuf and write rbuf over PCIe, only
 the part peers pull is staged in HBM.
 
@@ -29,7 +29,11 @@ def main():
     xh = (torch.rand(n) * 2 - 1).pin_memory()
     yh = torch.empty_like(xh).pin_memory()
     zc = os.environ.get("E2E_ZERO_COPY", "0") == "1"
-    fn = comm.allreduce_rabenseifner if zc else comm.allreduce_rabenseifner_host
+    rd = os.environ.get("E2E_ALGO", "raben") == "rd"
+    if rd:
+        fn = comm.recursive_doubling if zc else comm.recursive_doubling_host
+    else:
+        fn = comm.allreduce_rabenseifner if zc else comm.allreduce_rabenseifner_host
     for _ in range(2):
         assert fn(xh, yh) == 0
     ts = []
@@ -41,7 +45,7 @@ def main():
         ts.append(time.perf_counter() - t0)
     ts.sort()
     if rank == 0:
-        print(json.dumps({"ranks": int(os.environ["FTAR_SIZE"]), "count": n,
+        print(json.dumps({"algo": "rd" if rd else "raben", "ranks": int(os.environ["FTAR_SIZE"]), "count": n,
                           "host_pipe": os.environ.get("FTAR_HOST_PIPE", "1"), "zero_copy": zc,
                           "profiling": os.environ.get("FTAR_PROFILE", "0"),
                           "ms_median": round(ts[len(ts) // 2] * 1e3, 3), "ms_min": round(ts[0] * 1e3, 3)}), flush=True)
