@@ -177,7 +177,7 @@ def single(args):
                      "same_pair_kernel_ms": round(k_same, 4),
                      "same_pair_GBps": round(3 * S / (k_same * 1e-3) / 1e9, 1)},
     }
-    out["e2e"] = e2e_local(ftar, args.count)
+    out["e2e"] = e2e_local(ftar, args.count, args.variant)
     if args.no_cpu_baseline:
         out["cpu_baseline"] = None
     else:
@@ -189,7 +189,7 @@ def single(args):
     print(json.dumps(out), flush=True)
 
 
-def e2e_local(ftar, count, iters=5):
+def e2e_local(ftar, count, variant, iters=5):
     """Host-resident variant of the same step: pinned H2D of both vectors, the kernel,
     pinned D2H of the result (PCIe-bound), never the headline value."""
     import torch
@@ -221,8 +221,11 @@ def e2e_local(ftar, count, iters=5):
     # zero copy: the kernel reads both pinned host vectors and writes the result back
     # over PCIe in one pass -- reads and writes on the link's two directions at once
     # instead of H2D, kernel, D2H in turn (ftar_reduce_local accepts pinned host memory)
+    # (the register kernel, as fast here: the 10 ms PCIe-bound launches then stay out of
+    # the headline kernel's rocprof statistics)
     y0 = torch.rand(count)
     tz = 0.0
+    ftar.set_reduce_variant(0)
     for _ in range(iters):
         yh.copy_(y0)
         torch.cuda.synchronize()
@@ -230,6 +233,7 @@ def e2e_local(ftar, count, iters=5):
         ftar.reduce_local(xh, yh)
         torch.cuda.synchronize()
         tz += time.perf_counter() - t0
+    ftar.set_reduce_variant(variant)
     out["zero_copy"] = {"ms": round(tz * 1e3 / iters, 3), "GBps": round(2 * S * iters / tz / 1e9, 2),
                         "pcie_GBps": round(3 * S * iters / tz / 1e9, 2),
                         "exact": bool(torch.equal(yh, y0 + xh))}

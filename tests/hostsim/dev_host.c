@@ -254,7 +254,10 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
 }
 
 int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes) { return ptr == NULL; }
-int fdev_host_pinned(const void *ptr) { return 0; } /* host-sim: the _host entry points always stage */
+/* host-sim: "device" memory is host memory, so every buffer could be used in place; the
+ * _host entry points stage unless FTAR_HOSTSIM_PINNED=1 makes the caller's buffers count
+ * as pinned (the zero-copy route of the GPU build, tested with kills on CPU) */
+int fdev_host_pinned(const void *ptr) { return ptr && getenv("FTAR_HOSTSIM_PINNED") && atoi(getenv("FTAR_HOSTSIM_PINNED")); }
 
 int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
                     void *const *out, const size_t *n, int ntree, int tag)

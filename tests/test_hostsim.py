@@ -77,6 +77,27 @@ def test_single_kill_sweep(hostsim, oracle, algo, p):
     assert n > 0
 
 
+@pytest.mark.parametrize("algo,p", [("raben", 5), ("rd", 6), ("raben", 4)])
+def test_host_entry_zero_copy_kill_sweep(hostsim, oracle, algo, p):
+    """The _host entry points' zero-copy route (caller buffers pinned: the device entry
+    point runs on them in place) under every single kill point: same outcome class and
+    bit-identical survivor results as the oracle."""
+    ins = oracle.random_inputs(p, 257, seed=p + 40)
+    phases = [0, 1, 2, 3] if algo == "raben" else [0, 1, 3]
+    fn = _fn(oracle, algo)
+    n = 0
+    for v in range(p):
+        for ph in phases:
+            for st in range(3):
+                for pt in range(4):
+                    ks = [(v, ph, st, pt)]
+                    if fn(ins, ks).status[v] != oracle.DEAD:
+                        continue
+                    _cmp(fn, algo, ins, ks, env={"FTAR_HOSTSIM_PINNED": "1"})
+                    n += 1
+    assert n > 0
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_multi_kill_random(hostsim, oracle, seed):
     rng = random.Random(seed)
