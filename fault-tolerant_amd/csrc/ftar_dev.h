@@ -74,11 +74,14 @@ int fdev_import(ftar_dev *d, const void *handle, void **ptr);
  * it.  Nonzero if the memory cannot be shared (the caller then stages it). */
 int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, uint64_t *id, size_t *offset);
 int fdev_unimport(ftar_dev *d, void *ptr);
-/* 0 if the device can access [ptr, ptr + bytes): device memory inside one allocation,
- * or pinned / managed memory; nonzero for pageable host memory or a range past the end
- * of its allocation (the device entry points refuse those instead of faulting). */
+/* 0 if the device can access [ptr, ptr + bytes): this device's memory inside one
+ * allocation, pinned host memory mapped at its own address, or managed memory; nonzero
+ * for pageable host memory, another GPU's memory, host memory mapped elsewhere, or a
+ * range past the end of its allocation (the device entry points refuse those instead of
+ * faulting). */
 int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes);
-/* 1 if `ptr` is pinned host memory (the kernels read and write it in place over PCIe) */
+/* 1 if `ptr` is pinned host memory mapped into the device at its own address (the
+ * kernels can read and write it in place over PCIe) */
 int fdev_host_pinned(const void *ptr);
 
 /* Enqueue one segment kernel on the rank's stream. */
