@@ -140,10 +140,12 @@ int ftar_set_kills(ftar_comm *comm, const ftar_kill *kills, int nkills);
  * Device-resident, blocking (return when the result is in the output buffer).
  * `stream` ordering: the call first waits for all work queued on the stream set
  * with ftar_comm_set_stream (default: the null stream) to finish.
- * Buffers must be device-accessible for count elements (device memory, or pinned /
- * managed host memory): pageable host memory, or a range running past the end of its
- * allocation, returns FTAR_ERR_ARG before anything is launched (use the _host entry
- * points for host buffers).
+ * Buffers must be device-accessible for count elements: memory of the comm's GPU,
+ * managed memory, or pinned host memory mapped at its own address (hipHostMalloc, a
+ * pinned torch tensor), which this rank's kernels read and write in place over PCIe.
+ * Pageable host memory, another GPU's memory, or a range running past the end of its
+ * allocation returns FTAR_ERR_ARG before anything is launched (the _host entry points
+ * take any host buffer).
  */
 
 /* Fault-tolerant Rabenseifner Allreduce (raben/rabenseifner.c:3-395).
