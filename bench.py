@@ -806,7 +806,8 @@ def multi(args):
                                    f"rank, one rank per MI355X -- {schedule}",
                        "schedule": schedule, "transport": transport,
                        "step0_redundancy": "full exchange (reference)" if keep else
-                       "elided (no idle rank: every handler aborts, raben/errhandler.c:207-211)",
+                       "elided (no idle rank: every handler aborts, raben/errhandler.c:207-211; with a "
+                       "spare the replay reads the dead rank's step-0 half in its still-mapped IN)",
                        "count": args.count, "parallelism": f"{world} ranks"},
             "algbw_GBps": round(S / t_rb / 1e9, 2),
             "transport": transport,

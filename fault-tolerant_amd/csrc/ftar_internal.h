@@ -80,7 +80,7 @@ struct ftar_comm {
     int relay;           /* FTAR_RELAY (default 1): stripe exchanges over 2-hop paths */
     size_t relay_min;    /* FTAR_RELAY_MIN bytes: smallest per-rank window that is relayed */
     int copy_engine;     /* FTAR_COPY_ENGINE (default 0): direct pulls by hipMemcpyAsync */
-    int redundancy;      /* FTAR_REDUNDANCY (default 0 = only when a spare can use it) */
+    int redundancy;      /* FTAR_REDUNDANCY (default 0: the step-0 copy is never moved; a replay reads the dead rank's IN) */
     int mesh;            /* FTAR_MESH (default 1): one-hop Raben at power-of-two p without a spare */
     size_t oneshot_max;  /* FTAR_ONESHOT_MAX bytes: mesh Raben in one launch up to this size */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */

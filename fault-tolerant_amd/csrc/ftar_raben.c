@@ -8,7 +8,8 @@
  *
  *   RS step 0 (:206-211 full exchange + :231-237 reduce):
  *       W[rw0] = IN[rw0] + peer.IN[rw0]        (reduce half)
- *       T[sw0] = peer.IN[sw0]                  (redundancy copy for recovery)
+ *       T[sw0] = peer.IN[sw0]                  (redundancy copy, FTAR_REDUNDANCY=1 only:
+ *                                               a replay otherwise reads peer.IN itself)
  *   RS step k>=1 (:219-237):  W[rwk] = W[rwk] + peer.W[rwk]
  *   AG step k (:299-315):     W[swk] = peer.W[swk]
  *
@@ -49,6 +50,7 @@ typedef struct {
     int out_done;   /* the last allgather step already stored this rank's result in rbuf */
     int mesh;       /* fast_io on the full mesh: one-hop reduce-scatter and allgather */
     int oneshot;    /* mesh of a small vector: every block in its owner's tree, one launch */
+    int in0_w[FTAR_MAX_RANKS]; /* world rank whose IN held vrank v's input at RS step 0 */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
 } rb_ctx;
 
@@ -160,15 +162,22 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
         int64_t dri[MAXSTEPS], dsi[MAXSTEPS], drc[MAXSTEPS], dsc[MAXSTEPS];
         rb_windows(vdead, x->count, x->steps, dri, dsi, drc, dsc);
         if (x->rank == org) {
-            if (!x->has_recov) ftar_abort(c, 1); /* deviation: no step-0 copy to replay from */
+            if (!x->has_recov) ftar_abort(c, 1); /* deviation: a replacement holds no step-0 half */
             if (x->bg_pending) { /* the dead rank's half of its vector must be in T */
                 ftar_drain_bg(c);
                 x->bg_pending = 0;
             }
             /* replay the dead rank's steps 0..fs (:106-200) into W's half this rank sent at
-             * step 0 (= the dead rank's reduce window, unused here until the allgather) */
-            void *W = c->ws[WS_W], *IN = ftar_local(c, WS_IN), *T = c->ws[WS_T];
-            run_reduce(x, at(x, W, dri[0]), at(x, IN, dri[0]), at(x, T, dri[0]), drc[0], 0, FDEV_TAG_RECOV);
+             * step 0 (= the dead rank's reduce window, unused here until the allgather).
+             * The dead rank's step-0 half: the reference's tmp copy (:191-197) where it was
+             * made (FTAR_REDUNDANCY=1: T), else read where it lies -- the IN of the rank that
+             * held vrank vdead at step 0 stays mapped and unwritten after its death (the
+             * peers' mappings hold its memory), so the copy need not cross a link in every
+             * call to make a recovery possible. */
+            void *W = c->ws[WS_W], *IN = ftar_local(c, WS_IN);
+            const void *D0 = x->keep_recov ? (const void *)c->ws[WS_T] : ftar_buf(c, x->in0_w[vdead], WS_IN);
+            run_reduce(x, at(x, W, dri[0]), at(x, IN, dri[0]), at(x, (void *)D0, dri[0]), drc[0],
+                       x->keep_recov ? 0 : FDEV_REMOTE_Y, FDEV_TAG_RECOV);
             for (int s = 1; s <= fs; s++) {
                 int pw = c->order[rb_real(x, vdead ^ (1 << s))];
                 void *PW = ftar_buf(c, pw, WS_W);
@@ -441,8 +450,13 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * there is no idle spare (new_entry = 2 rem - 1 = -1, errhandler.c:207-211,377-378).
      * rem only decreases during a call, so with rem = 0 at the start the copy can never
      * be consumed: skip it (FTAR_REDUNDANCY=1 keeps it, the reference's shape). */
-    x->keep_recov = c->redundancy || x->rem > 0;
-    x->has_recov = x->keep_recov;
+    x->keep_recov = c->redundancy;
+    /* The reference's recovery data: every rank holds its step-0 partner's other half (in
+     * tmp) while a spare can use it, except a replacement rank (errhandler.c:213-241 ships
+     * it the dead rank's state, not its redundancy: a replay by it aborts, as the oracle's
+     * restatement does).  Without the physical copy (keep_recov = 0) the replay reads that
+     * half where it lies: the IN of the rank that held the vrank at step 0. */
+    x->has_recov = c->redundancy || x->rem > 0;
     /* Without an idle rank every failure aborts (new_entry = -1, errhandler.c:207-211,
      * 377-378), so nothing outside the schedule has to stay recoverable: step 0 reads
      * this rank's reduce half straight from sbuf (only the half peers pull is staged in
@@ -546,6 +560,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     if (x->mesh) return rb_mesh(x, sbuf, rbuf);
 
     /* ---- reduce-scatter (:170-284) ---- */
+    for (int v = 0; v < x->adjsize; v++) x->in0_w[v] = c->order[rb_real(x, v)];
     int step = 0;
     for (int mask = 1; mask < x->adjsize; mask <<= 1, step++) {
         ftar_plan P;
