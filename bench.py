@@ -17,7 +17,19 @@ N > 1: configs[3] -- fault-tolerant Rabenseifner Allreduce of a 256 MiB float32 
        (pairwise, step by step, step-0 full exchange) is timed as `reference_shape`.
        Recursive doubling (configs[2]), RCCL's all_reduce, a size sweep 4 B - 256 MiB
        (FT vs RCCL), the host-C CPU port of the schedule, and configs[4] (9 ranks = N
-       GPUs + one idle spare, a kill mid-exchange, recovery) are reported beside it.
+       GPUs + one idle spare, kills mid-exchange, recovery, a seeded random-kill
+       campaign) are reported beside it.
+
+The N > 1 run is built so that its first contact with a node cannot lose the headline:
+  * the side legs (CPU baseline, fabric probe, configs[4] jobs) share ONE time budget
+    (--side-budget) with a deadline per leg; a leg that overruns is killed (its own
+    process group) and recorded as a timeout;
+  * the headline JSON line is printed as soon as the configs[3] Allreduce is timed
+    ("line": "headline"), with its roofline and north-star verdict; every later leg is
+    optional, runs only while the job's budget (--budget) has room for it (decided
+    uniformly over ranks), records its own failure, and the enriched line is printed last
+    ("line": "final": the same keys plus the legs);
+  * a watchdog prints what exists and ends the rank if the budget is overrun anyway.
 
 value = (input vectors summed x bytes per vector) / time per step, whole job:
         N=1: 2 x 256 MiB per launch; N>1: N x 256 MiB per Allreduce.
@@ -27,17 +39,69 @@ import argparse
 import importlib.util
 import json
 import os
+import signal
 import subprocess
 import sys
+import threading
 import time
 
+T_START = time.monotonic()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 COUNT = 1 << 26              # 256 MiB of float32 per vector
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
-XGMI_LINK_GBS = 76.8         # one xGMI link, one direction (153.6 GB/s bidirectional spec)
+XGMI_LINK_GBS = 76.8         # nominal: one xGMI link, one direction (153.6 GB/s bidirectional spec)
+SURVEY_LINK_GBS = 153.6      # SURVEY.md 8d's nominal B_link "per direction" (assumption to confirm)
+NORTH_STAR_FRAC = 0.70       # BASELINE.json north_star: >= 70 % of the xGMI-bound roofline at 8 GPUs
 METRIC = "Allreduce GB/s (device-resident, float32 SUM) at 1/2/4/8 MI355X"
 # data/data_fault/log_single_Raben.csv, N = 9, OK runs: median clock() seconds
 REF_C5_S = {"kill": 1.334, "no_kill": 1.329, "count": 120732254}
+
+
+class LegTimeout(RuntimeError):
+    pass
+
+
+def left(deadline):
+    return deadline - time.monotonic()
+
+
+def run_proc(cmd, timeout, env=None, cwd=None):
+    """Run `cmd` in a session of its own and wait at most `timeout` s; past it the whole
+    process group (the job's launcher and every rank it forked) is SIGKILLed.  Returns
+    (rc, stdout, stderr, timed_out)."""
+    p = subprocess.Popen(cmd, env=env, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=max(0.5, timeout))
+        return p.returncode, out, err, False
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)  # the group this call created, nothing else
+        except ProcessLookupError:
+            pass
+        out, err = p.communicate()
+        return p.returncode, out, err, True
+
+
+def test_hook(kind, leg):
+    """TEST-ONLY fault hooks for the bench's own robustness tests (tests/test_bench_logic.py,
+    tests/test_gpu_bench.py): FTAR_BENCH_HANG=<side leg> replaces that leg by a stand-in
+    job that never ends; FTAR_BENCH_FAIL=<leg>[,<leg>...] makes that leg raise (on every
+    rank at once).  Unset in every measured run."""
+    v = os.environ.get("FTAR_BENCH_HANG" if kind == "hang" else "FTAR_BENCH_FAIL", "")
+    return leg in [s.strip() for s in v.split(",") if s.strip()]
+
+
+def maybe_hang(leg, deadline):
+    if test_hook("hang", leg):
+        rc, _, _, to = run_proc(["sleep", "3600"], left(deadline))
+        if to:
+            raise LegTimeout(f"{leg}: stand-in job still running at its deadline (killed)")
+
+
+def maybe_fail(leg):
+    if test_hook("fail", leg):
+        raise RuntimeError(f"{leg}: forced failure (FTAR_BENCH_FAIL)")
 
 
 def load_package():
@@ -89,19 +153,19 @@ def cpu_baseline_local_reduce(min_seconds=10.0, max_passes=2000):
                       f"({dt:.1f} s), 1 host thread"}
 
 
-def cpu_schedule(algo, p, count, reps):
+def cpu_schedule(algo, p, count, reps, timeout=600.0):
     """The schedule on the host cores: the product's host C (control plane, agree rounds,
     the FT schedule) as p processes pinned one per core, POSIX shared memory as the
     transport, C loops as the reduce (tools/cpu_schedule_bench.py), float32."""
     cs = load_tool("cpu_schedule_bench")
     cs.build()
-    r = cs.run(algo, p, count, "float32", reps)
+    r = cs.run(algo, p, count, "float32", reps, timeout=timeout)
     return r, cs.cpu_model()
 
 
-def c1_baseline():
+def c1_baseline(timeout=120.0):
     """BASELINE configs[0]: src/rd/main recursive doubling, float32 SUM, 64 KiB, 4 ranks."""
-    r, model = cpu_schedule("rd", 4, 16384, 20)
+    r, model = cpu_schedule("rd", 4, 16384, 20, timeout=timeout)
     return {"value": round(4 * 16384 * 4 / r["time_s"] / 1e9, 4), "unit": "GB/s", "ms_per_call": round(r["time_s"] * 1e3, 4),
             "algbw_GBps": r["algbw_GBps"], "cores": 4, "kind": "port", "cpu_model": model,
             "sample": "configs[0]: recursive doubling, 64 KiB float32 SUM per rank, 4 rank processes pinned one "
@@ -240,37 +304,61 @@ def e2e_local(ftar, count, variant, iters=5):
     return out
 
 
-def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
+# ---- configs[4]: its own ftrun jobs (torchrun's agent tears a job down on a SIGKILL) ----
+
+def _c5_env():
+    return {k: v for k, v in os.environ.items()
+            if not k.startswith(("FTAR_", "RANK", "LOCAL_", "WORLD_", "GROUP_", "ROLE_", "TORCHELASTIC"))}
+
+
+def _ftrun_paths():
+    return (os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftrun"),
+            os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftbench"))
+
+
+def _mid_exchange_lines(stderr):
+    """ftrun's post-mortem of every rank killed by a signal (the victim's control slot: was a
+    kernel of its exchange in flight when it died?) and the DURING victim's own line."""
+    return [l.split("ftrun: ")[-1] if "ftrun: " in l else l.split("ftar: ")[-1]
+            for l in stderr.splitlines() if "mid-exchange" in l or "killed by signal" in l]
+
+
+def c5_leg(world, devices, count, ranks, deadline, calls=6, kill_call=2):
     """configs[4] on this node: `ranks` = world GPUs' worth of ranks + one idle spare (rank
     1 shares rank 0's GPU), Rabenseifner 256 MiB float32 SUM, `calls` calls per job; the
     fault job kills vrank 5 (original rank 6) in reduce-scatter step 1 of call `kill_call`,
     mid-exchange (its own pull kernel in flight, its partner's pull reading its HBM), a
     second one in allgather step 1 ("also AG step 1"; the last AG step when
-    there are only two).  The recovery shrinks the comm; the later calls run on the
-    survivors.  Call 0 is the warm-up (workspace allocation, IPC imports).  Run by rank 0
-    as separate ftrun jobs of bin/ftbench: torchrun's agent would tear the job down on a
-    SIGKILL."""
-    exe = os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftbench")
-    ftrun = os.path.join(ROOT, "fault-tolerant_amd", "bin", "ftrun")
+    there are only two).  Every job runs in both recovery shapes: the default (no step-0
+    redundancy copy; the replay reads the dead rank's step-0 half in its still-mapped IN)
+    and the reference's (FTAR_REDUNDANCY=1: the copy moves in every call and the replay
+    reads it, raben/rabenseifner.c:206-211).  The recovery shrinks the comm; the later
+    calls run on the survivors.  Call 0 is the warm-up (workspace allocation, IPC
+    imports).  Every job ends by `deadline` (killed past it)."""
+    ftrun, exe = _ftrun_paths()
     devmap = [devices[0], devices[0]] + [devices[(r - 1) % len(devices)] for r in range(2, ranks)]
     victim = 6 if ranks > 6 else ranks - 1
     ag_step = 1 if ranks >= 8 else 0  # a middle allgather step where there is one (L >= 3)
-    env = {k: v for k, v in os.environ.items()
-           if not k.startswith(("FTAR_", "RANK", "LOCAL_", "WORLD_", "GROUP_", "ROLE_", "TORCHELASTIC"))}
+    env = _c5_env()
     res = {"ranks": ranks, "devmap": devmap, "count": count, "calls": calls,
            "kill": f"{victim}:1:1:3 in call {kill_call} (original rank {victim} = vrank {victim - 1}, reduce-scatter "
                    "step 1, mid-exchange)",
            "kill_ag": f"{victim}:2:{ag_step}:3 in call {kill_call} (allgather step {ag_step}, mid-exchange)"}
     want_all = float(sum(range(ranks)))
-    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}"),
-                       ("fault_ag", f"{victim}:2:{ag_step}:3:{kill_call}")):
+
+    def job(kill, redundancy):
         e = dict(env)
         if kill:
             e["FTAR_KILL"] = kill
+        if redundancy:
+            e["FTAR_REDUNDANCY"] = "1"
         t0 = time.time()
-        cp = subprocess.run([ftrun, "-np", str(ranks), "--devmap", ",".join(map(str, devmap)), exe, "raben",
-                             str(count), str(calls)], env=e, capture_output=True, text=True, timeout=180)
-        lines = [json.loads(l) for l in cp.stdout.splitlines() if l.startswith("{")]
+        rem = left(deadline)
+        if rem < 1.0:
+            return {"skipped": "side-leg budget spent"}
+        rc, out, err, to = run_proc([ftrun, "-np", str(ranks), "--devmap", ",".join(map(str, devmap)), exe, "raben",
+                                     str(count), str(calls)], min(rem, 120.0), env=e)
+        lines = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
         per_call = []
         for c in range(calls):
             per = [ln["calls"][c] for ln in lines]
@@ -282,60 +370,107 @@ def c5_leg(world, devices, count, ranks, calls=6, kill_call=2):
                              "comm_size_after": min((p["comm_size"] for p in per), default=None),
                              "result_ok": bool(per) and all(p["rc"] == 0 and p["uniform"] and p["value"] == want
                                                             for p in per)})
-        res[name] = {"rc": cp.returncode, "survivors": len(lines), "job_wall_s": round(time.time() - t0, 2),
-                     "calls": per_call}
-        if cp.returncode != 0 or not lines:
-            res[name]["stderr_tail"] = cp.stderr[-600:]
-        mid = [l for l in cp.stderr.splitlines() if "dies mid-exchange" in l]
+        r = {"rc": rc, "survivors": len(lines), "job_wall_s": round(time.time() - t0, 2), "calls": per_call}
+        if to:
+            r["timed_out"] = True
+        if rc != 0 or not lines:
+            r["stderr_tail"] = err[-600:]
+        mid = [l for l in err.splitlines() if "dies mid-exchange" in l]
         if mid:
-            res[name]["victim"] = mid[0].split("ftar: ")[-1]
-    res["random_kill"] = c5_random_kill(ftrun, exe, ranks, devmap, count, env)
-    f, n = res.get("fault", {}), res.get("no_fault", {})
+            r["victim"] = mid[0].split("ftar: ")[-1]
+        return r
 
     def med(cs):
-        v = sorted(c["ms_max_over_ranks"] for c in cs)
-        return v[len(v) // 2]
-    def recovered(job):
-        fc = job["calls"]
-        return job["survivors"] == ranks - 1 and fc[kill_call]["recoveries"] == 1 and all(c["result_ok"] for c in fc)
-    try:
-        fc = f["calls"]
-        res["recovered_rs"] = recovered(f)
-        res["recovered_ag"] = recovered(res["fault_ag"])
-        res["recovered"] = res["recovered_rs"] and res["recovered_ag"]
-        res["recovered_call_ms"] = fc[kill_call]["ms_max_over_ranks"]
-        res["recovered_ag_call_ms"] = res["fault_ag"]["calls"][kill_call]["ms_max_over_ranks"]
-        res["no_fault_call_ms"] = med(n["calls"][1:])  # median after the warm-up call
-        res["recovery_overhead_ms"] = round(res["recovered_call_ms"] - res["no_fault_call_ms"], 3)
-        res["pre_fault_call_ms"] = med(fc[1:kill_call])
-        res["survivors_call_ms"] = med(fc[kill_call + 1:])  # p - 1 ranks after the shrink
-    except (KeyError, IndexError, TypeError, ValueError):
-        res["recovered"] = False
+        v = sorted(c["ms_max_over_ranks"] for c in cs if c["ms_max_over_ranks"] is not None)
+        return v[len(v) // 2] if v else None
+
+    def recovered(j):
+        fc = j.get("calls")
+        return bool(fc) and j["survivors"] == ranks - 1 and fc[kill_call]["recoveries"] == 1 and \
+            all(c["result_ok"] for c in fc)
+
+    def summarize(n, f, fa):
+        s = {}
+        try:
+            s["recovered_rs"] = recovered(f)
+            s["recovered_ag"] = recovered(fa)
+            s["recovered"] = s["recovered_rs"] and s["recovered_ag"]
+            fc = f["calls"]
+            s["recovered_call_ms"] = fc[kill_call]["ms_max_over_ranks"]
+            s["recovered_ag_call_ms"] = fa["calls"][kill_call]["ms_max_over_ranks"]
+            s["no_fault_call_ms"] = med(n["calls"][1:])  # median after the warm-up call
+            s["recovery_overhead_ms"] = round(s["recovered_call_ms"] - s["no_fault_call_ms"], 3)
+            s["pre_fault_call_ms"] = med(fc[1:kill_call])
+            s["survivors_call_ms"] = med(fc[kill_call + 1:])  # p - 1 ranks after the shrink
+        except (KeyError, IndexError, TypeError, ValueError):
+            s["recovered"] = False
+        return s
+
+    maybe_hang("c5", deadline)
+    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}"),
+                       ("fault_ag", f"{victim}:2:{ag_step}:3:{kill_call}")):
+        res[name] = job(kill, False)
+    res.update(summarize(res["no_fault"], res["fault"], res["fault_ag"]))
+    ref = {"shape": "FTAR_REDUNDANCY=1: the step-0 copy of the partner's other half moves in every call and the RS "
+                    "replay reads it (raben/rabenseifner.c:206-211, raben/errhandler.c:106-200)"}
+    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}"),
+                       ("fault_ag", f"{victim}:2:{ag_step}:3:{kill_call}")):
+        ref[name] = job(kill, True)
+    ref.update(summarize(ref["no_fault"], ref["fault"], ref["fault_ag"]))
+    res["recovery_shape"] = ("default: no step-0 redundancy copy; the RS replay reads the dead rank's step-0 half in "
+                             "its IN, still mapped by the peers (DESIGN.md 3, deviation 6)")
+    res["reference_shape"] = ref
     res["reference_leonardo_s"] = dict(REF_C5_S, note="clock() s per run incl. the whole MPI job, 460.6 MiB int32")
     return res
 
 
-def c5_random_kill(ftrun, exe, ranks, devmap, count, env, calls=3, loop_s=1.5, seed=0):
-    """The reference's random kill (run/kill_procs.sh: SIGKILL one rank process after a
-    random delay) on the configs[4] job: each call is stretched to `loop_s` seconds of
-    busy agree rounds (FTAR_LOOP_SECONDS, as run/run_mpi.sh does) so the kill lands inside
-    the schedule; the outcome is the reference's (recovered, or MPI_Abort where its
-    handler aborts), and every survivor's results must agree, call by call, on the exact
-    sum with or without the victim's input, never dropping it and taking it back."""
+def reference_outcomes(n):
+    """The reference's recorded single-kill outcomes at N = n (tests/golden/ref_fault_outcomes.csv,
+    from data/data_fault/log_single_Raben.csv): recovered / MPI_Abort / deadlock."""
+    path = os.path.join(ROOT, "tests", "golden", "ref_fault_outcomes.csv")
+    out = {"recovered": 0, "aborted": 0, "deadlock": 0, "wrong": 0,
+           "source": "data/data_fault/log_single_Raben.csv via tests/golden/ref_fault_outcomes.csv"}
+    try:
+        for line in open(path).read().splitlines()[1:]:
+            algo, N, killed, abort, dead, right, cnt = line.split(";")
+            if algo != "raben" or int(N) != n or int(killed) == 0:
+                continue
+            if abort == "True":
+                out["aborted"] += int(cnt)
+            elif dead == "True":
+                out["deadlock"] += int(cnt)
+            elif right == "True":
+                out["recovered"] += int(cnt)
+            else:
+                out["wrong"] += int(cnt)
+    except (OSError, ValueError):
+        return None
+    return out
+
+
+def c5_random_kill(ftrun, exe, ranks, devmap, count, env, deadline, calls=3, loop_s=1.5, seed=0):
+    """One draw of the reference's random kill (run/kill_procs.sh: SIGKILL one rank process
+    after a random delay) on the configs[4] job.  Each call is stretched to `loop_s` seconds
+    (FTAR_LOOP_SECONDS, as run/run_mpi.sh does) with idempotent re-pulls of the step's
+    window, so the kill lands while exchange kernels are in flight; ftrun's post-mortem
+    says whether the victim died with one in flight.  The outcome is the reference's
+    (recovered, or MPI_Abort where its handler aborts), and every survivor's results must
+    agree, call by call, on the exact sum with or without the victim's input, never
+    dropping it and taking it back."""
     import random
-    import signal
     rng = random.Random(seed)
     victim = rng.randrange(ranks)
-    delay = rng.uniform(1.0, 1.0 + loop_s * calls)  # after the launch: ~1 s of process start-up
+    delay = rng.uniform(1.5, 1.0 + loop_s * calls)  # after the launch: ~1 s of process start-up
     e = dict(env, FTAR_LOOP_SECONDS=str(loop_s))
-    out = {"victim": victim, "delay_s": round(delay, 3), "loop_seconds": loop_s, "calls": calls}
+    out = {"seed": seed, "victim": victim, "delay_s": round(delay, 3), "loop_seconds": loop_s, "calls": calls}
     pr = None
     try:
         import psutil
         t0 = time.time()
         pr = subprocess.Popen([ftrun, "-np", str(ranks), "--devmap", ",".join(map(str, devmap)), exe, "raben",
-                               str(count), str(calls)], env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-        time.sleep(delay)
+                               str(count), str(calls)], env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True, start_new_session=True)
+        time.sleep(min(delay, max(0.0, left(deadline) - 1.0)))
         for k in psutil.Process(pr.pid).children():  # the rank processes ftrun started
             try:
                 if k.environ().get("FTAR_RANK") == str(victim):
@@ -343,18 +478,28 @@ def c5_random_kill(ftrun, exe, ranks, devmap, count, env, calls=3, loop_s=1.5, s
                     out["killed"] = True
             except (psutil.Error, OSError):
                 pass
-        so, se = pr.communicate(timeout=180)
+        so, se = pr.communicate(timeout=max(1.0, min(60.0, left(deadline))))
         out["job_wall_s"] = round(time.time() - t0, 2)
+        out["rc"] = pr.returncode
+    except subprocess.TimeoutExpired:
+        os.killpg(pr.pid, signal.SIGKILL)
+        pr.communicate()
+        out["outcome"] = "lost"
+        out["error"] = "job still running at its deadline (deadlock?): killed"
+        return out
     except Exception as ex:
         out["error"] = str(ex)[-300:]
+        out["outcome"] = "error"
         if pr is not None and pr.poll() is None:
-            pr.kill()  # ftrun's ranks follow it (PR_SET_PDEATHSIG)
+            os.killpg(pr.pid, signal.SIGKILL)
             pr.wait()
         return out
     lines = [json.loads(l) for l in so.splitlines() if l.startswith("{")]
     full = float(sum(range(ranks)))
     out["aborted"] = "MPI_ABORT" in se
     out["survivors"] = len(lines)
+    out["post_mortem"] = _mid_exchange_lines(se)
+    out["mid_exchange"] = any("killed by signal" in l and "mid-exchange" in l for l in out["post_mortem"])
     consistent = bool(lines) or out["aborted"]
     dropped = False
     per = []
@@ -364,17 +509,49 @@ def c5_random_kill(ftrun, exe, ranks, devmap, count, env, calls=3, loop_s=1.5, s
         v = vals.pop() if len(vals) == 1 else None
         if v is not None and v not in (full, full - victim):
             ok = False
-        if dropped and v == full:
+        if dropped and v == full and victim != 0:  # (rank 0's input is 0: both sums coincide)
             ok = False
         dropped = dropped or v == full - victim
         consistent = consistent and ok
         per.append({"value": v, "recoveries": max((ln["calls"][c]["recoveries"] for ln in lines), default=None),
                     "ms_max_over_ranks": round(max((ln["calls"][c]["ms"] for ln in lines), default=0.0), 3)})
     out["per_call"] = per
-    out["outcome"] = "aborted" if out["aborted"] else "recovered" if len(lines) == ranks - 1 else \
-        "no fault hit" if len(lines) == ranks else "lost"
     out["results_consistent"] = consistent
+    if not lines and not out["aborted"]:
+        # no survivor printed and nobody called MPI_Abort: the job itself failed
+        out["outcome"] = "failed"
+        out["stderr_tail"] = se[-400:]
+    elif not consistent:
+        out["outcome"] = "wrong"
+        out["ranks_calls"] = [[(c["rc"], c["value"], c["uniform"], c["recoveries"], c["comm_size"]) for c in ln["calls"]]
+                              for ln in lines]
+        out["stderr_tail"] = se[-1500:]
+    else:
+        out["outcome"] = "aborted" if out["aborted"] else "recovered" if len(lines) == ranks - 1 else \
+            "no fault hit" if len(lines) == ranks else "lost"
     return out
+
+
+def c5_campaign(devices, count, ranks, deadline, draws=10, seed0=0):
+    """configs[4]'s random-kill campaign: up to `draws` seeded draws (victim, delay) of
+    c5_random_kill at `ranks` ranks while the side-leg budget lasts, with the outcome counts
+    next to the reference's own at N = 9."""
+    ftrun, exe = _ftrun_paths()
+    devmap = [devices[0], devices[0]] + [devices[(r - 1) % len(devices)] for r in range(2, ranks)]
+    maybe_hang("c5_campaign", deadline)
+    runs = []
+    for k in range(draws):
+        if left(deadline) < 9.0:  # a draw takes ~5-7 s: start none that cannot finish
+            break
+        runs.append(c5_random_kill(ftrun, exe, ranks, devmap, count, _c5_env(), deadline, seed=seed0 + k))
+    counts = {}
+    for r in runs:
+        counts[r.get("outcome", "error")] = counts.get(r.get("outcome", "error"), 0) + 1
+    killed = [r for r in runs if r.get("killed")]
+    return {"ranks": ranks, "count": count, "draws_planned": draws, "draws_run": len(runs), "outcomes": counts,
+            "mid_exchange_kills": sum(1 for r in killed if r.get("mid_exchange")), "kills": len(killed),
+            "wrong": counts.get("wrong", 0), "lost": counts.get("lost", 0),
+            "reference_single_kill_N9": reference_outcomes(9), "runs": runs}
 
 
 def leg_flag(tag):
@@ -385,89 +562,206 @@ def leg_flag(tag):
 
 def side_legs(args, rank, world, devices, rehearsal):
     """The legs rank 0 runs as other processes -- the CPU baseline (host processes), the
-    configs[4] jobs (ftrun, 9 ranks) and the fabric probe (one process on every GPU) --
+    fabric probe (one process on every GPU) and the configs[4] jobs (ftrun, 9 ranks) --
     BEFORE any torchrun rank touches a GPU: the other ranks wait here on a flag file
-    without having imported torch.  Run after the main legs they would share the cards
-    with the job's own ranks (8 + 9 GPU processes at N = 8, beyond what a box lets one
-    job run on a card).  Returns (cpu, c5, xgmi) on rank 0, Nones elsewhere."""
+    (importing torch opens no GPU: tools/kfd_probe.py).  Run after the main legs they would
+    share the cards with the job's own ranks (8 + 9 GPU processes at N = 8, beyond what a
+    box lets one job run on a card).  All of them share ONE budget (args.side_budget s):
+    each leg gets a deadline carved out of what is left, a leg past its deadline is killed
+    and recorded, and the flag is written whatever happens.  Returns (cpu, c5, xgmi, info)
+    on rank 0, Nones elsewhere."""
     flag = leg_flag("side")
     if rank != 0:
-        while not os.path.exists(flag):
+        limit = time.monotonic() + args.side_budget + 60.0
+        while not os.path.exists(flag) and time.monotonic() < limit:
             time.sleep(0.05)
-        return None, None, None
+        return None, None, None, None
     S = args.count * 4
     cpu = c5 = xgmi = None
+    end = time.monotonic() + args.side_budget
+    info = {"budget_s": args.side_budget}
+
+    def leg(name, share, fn):
+        d = min(end, time.monotonic() + share * args.side_budget)
+        t0 = time.monotonic()
+        try:
+            if left(d) < 1.0:
+                raise LegTimeout("no budget left")
+            r = fn(d)
+            status = "ok"
+        except LegTimeout as e:
+            r, status = {"error": str(e)[-300:]}, "timeout"
+        except Exception as e:  # recorded, never fatal: the line stands without this leg
+            r, status = {"error": str(e)[-500:]}, "error"
+        info[name] = {"status": status, "s": round(time.monotonic() - t0, 2), "deadline_s": round(d - t0, 1)}
+        return r
+
+    def cpu_leg(d):
+        # the same schedule on this node's host cores, float32, 256 MiB per rank
+        maybe_hang("cpu_baseline", d)
+        r, model = cpu_schedule("raben", world, args.count, 3, timeout=left(d))
+        return {"value": round(world * S / r["time_s"] / 1e9, 4), "unit": "GB/s", "cores": world,
+                "kind": "port", "cpu_model": model, "ms_per_call": round(r["time_s"] * 1e3, 2),
+                "algbw_GBps": r["algbw_GBps"],
+                # the reference's TIME is clock() of one rank: CPU seconds per rank
+                # process (ranks spin, so it tracks wall time; it also covers init,
+                # fill, checksum)
+                "cpu_s_per_rank_process": r["cpu_s_per_rank_whole_process"],
+                "sample": f"Rabenseifner (FT, the reference's step-by-step pairwise shape), {world} rank "
+                          f"processes pinned one per core, 256 MiB float32 per rank through shared memory, "
+                          f"median of 3 calls (driver Time: lines, max over ranks); value = {world} x 256 MiB "
+                          f"/ call time"}
+
+    def xgmi_leg(d):
+        # the fabric (tools/xgmi_probe.hip, one process driving the job's GPUs): one link
+        # one way and both ways (SURVEY.md 8d's B_link), pull vs push, copy engines, the
+        # mesh's all-peers pattern; loopback in a one-GPU rehearsal
+        maybe_hang("xgmi_probe", d)
+        exe = os.path.join(ROOT, "tools", "_build", "xgmi_probe")
+        rc, out, err, to = run_proc([exe, str(1 if rehearsal else world)], left(d))
+        if to:
+            raise LegTimeout("xgmi_probe still running at its deadline (killed)")
+        lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+        return json.loads(lines[-1]) if lines else {"error": (err or out)[-300:], "rc": rc}
+
     try:
         if not args.no_cpu_baseline:
-            # the same schedule on this node's host cores, float32, 256 MiB per rank
-            try:
-                r, model = cpu_schedule("raben", world, args.count, 3)
-                cpu = {"value": round(world * S / r["time_s"] / 1e9, 4), "unit": "GB/s", "cores": world,
-                       "kind": "port", "cpu_model": model, "ms_per_call": round(r["time_s"] * 1e3, 2),
-                       "algbw_GBps": r["algbw_GBps"],
-                       # the reference's TIME is clock() of one rank: CPU seconds per rank
-                       # process (ranks spin, so it tracks wall time; it also covers init,
-                       # fill, checksum)
-                       "cpu_s_per_rank_process": r["cpu_s_per_rank_whole_process"],
-                       "sample": f"Rabenseifner (FT, the reference's step-by-step pairwise shape), {world} rank "
-                                 f"processes pinned one per core, 256 MiB float32 per rank through shared memory, "
-                                 f"median of 3 calls (driver Time: lines, max over ranks); value = {world} x 256 MiB "
-                                 f"/ call time"}
-            except Exception as e:
+            cpu = leg("cpu_baseline", 0.2, cpu_leg)
+            if "error" in cpu:
                 cpu = {"value": None, "unit": "GB/s", "cores": world, "kind": "port",
-                       "sample": f"failed: {str(e)[-300:]}"}
+                       "sample": f"failed: {cpu['error']}"}
+        if not args.no_xgmi:
+            xgmi = leg("xgmi_probe", 0.2, xgmi_leg)
         if not args.no_c5:
             # configs[4]: N GPUs' worth of ranks + the idle spare, its own ftrun jobs
-            try:
-                c5 = c5_leg(world, devices, args.count, int(os.environ.get("FTAR_C5_RANKS", "9")))
-            except Exception as e:
-                c5 = {"error": str(e)[-500:]}
-        if not args.no_xgmi:
-            # the fabric (tools/xgmi_probe.hip, one process driving the job's GPUs): one
-            # link one way and both ways (SURVEY.md 8d's B_link), pull vs push, copy
-            # engines, the mesh's all-peers pattern; loopback in a one-GPU rehearsal
-            exe = os.path.join(ROOT, "tools", "_build", "xgmi_probe")
-            try:
-                cp = subprocess.run([exe, str(1 if rehearsal else world)], capture_output=True, text=True,
-                                    timeout=240)
-                lines = [ln for ln in cp.stdout.splitlines() if ln.startswith("{")]
-                xgmi = json.loads(lines[-1]) if lines else {"error": (cp.stderr or cp.stdout)[-300:],
-                                                            "rc": cp.returncode}
-            except Exception as e:
-                xgmi = {"error": str(e)[-300:]}
+            ranks = int(os.environ.get("FTAR_C5_RANKS", "9"))
+            c5 = leg("c5", 0.35, lambda d: c5_leg(world, devices, args.count, ranks, d))
+            camp = leg("c5_campaign", 1.0, lambda d: c5_campaign(devices, args.count, ranks, d,
+                                                                 draws=args.c5_draws))
+            if isinstance(c5, dict):
+                c5["random_kill_campaign"] = camp
     finally:
+        info["total_s"] = round(args.side_budget - left(end), 2)
         with open(flag, "w") as f:
             f.write("done")
-    return cpu, c5, xgmi
+    return cpu, c5, xgmi, info
+
+
+class Watchdog(threading.Thread):
+    """Last resort against a hang the per-leg deadlines cannot reach (a collective stuck
+    on one rank): at `limit` s after the start rank 0 prints the line as it stands
+    ("truncated") and every rank exits.  Rank 0 fires first so it prints before a peer's
+    exit can abort the job."""
+
+    def __init__(self, limit, rank):
+        super().__init__(daemon=True)
+        self.limit = limit + (0.0 if rank == 0 else 5.0)
+        self.rank = rank
+        self.line = None
+        self.done = threading.Event()
+
+    def run(self):
+        if self.done.wait(max(0.0, self.limit - (time.monotonic() - T_START))):
+            return
+        if self.rank == 0 and self.line is not None:
+            d = dict(self.line, line="final", truncated=f"watchdog: the job passed its {self.limit:.0f} s budget; "
+                                                        "legs missing here did not finish")
+            print(json.dumps(d), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0 if self.line is not None else 3)
+
+
+def north_star_block(world, S, t_head, transport, link_gbps, links, head_bytes_per_link, t_ref=None, rehearsal=False):
+    """BASELINE.json north_star / SURVEY.md 8d: >= 70 % of the xGMI-bound roofline for the
+    device-resident Rabenseifner Allreduce of 256 MiB float32 at 8 GPUs.  SURVEY's roofline
+    is the FT schedule's data movement over one link per step, (2.5 - 2^(1-L)) S per rank
+    and direction (2.25 S at p = 8), priced at the calibrated single-link rate (B_link, both
+    directions loaded); the nominal 76.8 / 153.6 GB/s per direction are kept beside it as
+    assumptions.  Also priced: the bound of the schedule that ran (e.g. the one-hop mesh:
+    2 S / p over each of p - 1 links at once), which is the stricter yardstick."""
+    L = world.bit_length() - 1
+    ft_bytes = (2.5 - 2.0 ** (1 - L)) * S
+    priced = {}
+    for tag, b in (("calibrated", link_gbps), ("nominal_76.8_assumed", XGMI_LINK_GBS),
+                   ("survey_153.6_assumed", SURVEY_LINK_GBS)):
+        if not b:
+            continue
+        t_roof = ft_bytes / (b * 1e9)
+        t_sched = head_bytes_per_link / (b * 1e9)
+        row = {"link_GBps": round(b, 2), "t_roof_ms": round(t_roof * 1e3, 4),
+               "algbw_roof_GBps": round(S / t_roof / 1e9, 2),
+               "target_algbw_GBps": round(NORTH_STAR_FRAC * S / t_roof / 1e9, 2),
+               "frac": round(t_roof / t_head, 4), "met": t_roof / t_head >= NORTH_STAR_FRAC,
+               "schedule_t_roof_ms": round(t_sched * 1e3, 4), "schedule_frac": round(t_sched / t_head, 4)}
+        if t_ref:
+            row["reference_shape"] = {"frac": round(t_roof / t_ref, 4), "met": t_roof / t_ref >= NORTH_STAR_FRAC}
+        priced[tag] = row
+    basis = "calibrated" if "calibrated" in priced else "survey_153.6_assumed"
+    if rehearsal:  # every rank on one GPU: no link in the path, fractions would mix yardsticks
+        for row in priced.values():
+            for k in ("frac", "met", "schedule_frac"):
+                row[k] = None
+            if "reference_shape" in row:
+                row["reference_shape"] = {"frac": None, "met": None}
+    out = {"target": f">= {NORTH_STAR_FRAC:.0%} of SURVEY.md 8d's xGMI roofline for FT Rabenseifner, 256 MiB float32 "
+                     f"SUM, 8 GPUs", "applies": world == 8, "n_gpus": world,
+           "roofline_definition": f"(2.5 - 2^(1-L)) S = {ft_bytes:.0f} B per rank and direction over one link per step "
+                                  "(the reference's FT schedule), at B_link",
+           "schedule": transport, "schedule_bytes_per_link": head_bytes_per_link, "schedule_links": links,
+           "algbw_GBps": round(S / t_head / 1e9, 2), "ms_per_step": round(t_head * 1e3, 4),
+           "basis": basis, "frac": priced[basis]["frac"], "met": priced[basis]["met"], "priced": priced,
+           "rehearsal": rehearsal}
+    if t_ref:
+        out["reference_shape_ms"] = round(t_ref * 1e3, 4)
+        out["reference_shape_met"] = priced[basis]["reference_shape"]["met"]
+    return out
 
 
 def multi(args):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    cpu_mode = args.device == "cpu"
+    if cpu_mode and os.environ.get("FTAR_BENCH_CPU_TEST") != "1":
+        raise SystemExit("--device cpu is the bench's own CPU test (FTAR_BENCH_CPU_TEST=1), never a measurement")
     # FTAR_DEVICE pins every rank to one GPU (single-GPU rehearsal of the multi-rank path;
     # RCCL refuses two ranks on one device, so such runs use --dist-backend gloo)
-    rehearsal = "FTAR_DEVICE" in os.environ  # every rank on one GPU
+    rehearsal = "FTAR_DEVICE" in os.environ or cpu_mode  # every rank on one GPU
     # this job's GPUs (LOCAL_RANK = GPU on one node), or the one GPU of a rehearsal
-    devices = [int(os.environ["FTAR_DEVICE"])] if rehearsal else list(range(world))
-    cpu, c5, xgmi = side_legs(args, rank, world, devices, rehearsal)
+    devices = [int(os.environ.get("FTAR_DEVICE", "0"))] if rehearsal else list(range(world))
+    dog = Watchdog(args.budget, rank)
+    dog.start()
+    # torch is imported while rank 0 runs the side legs (the import opens no GPU device)
+    imp = threading.Thread(target=lambda: importlib.import_module("torch"), daemon=True)
+    imp.start()
+    cpu, c5, xgmi, side_info = side_legs(args, rank, world, devices, rehearsal)
+    imp.join()
     import torch
     import torch.distributed as dist
     ftar = load_package()
-    dev = int(os.environ.get("FTAR_DEVICE", local)) % max(1, torch.cuda.device_count())
-    os.environ.setdefault("FTAR_DEVICE", str(dev))  # the library opens the same device
-    torch.cuda.set_device(dev)
+    if cpu_mode:  # TEST-ONLY: the product's host C on host memory (tests/hostsim), no GPU
+        ftar.use_test_library(os.path.join(ROOT, "tests", "hostsim", "_build", "libftar_hostsim.so"))
+        dev = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
+    else:
+        dev_i = int(os.environ.get("FTAR_DEVICE", local)) % max(1, torch.cuda.device_count())
+        os.environ.setdefault("FTAR_DEVICE", str(dev_i))  # the library opens the same device
+        torch.cuda.set_device(dev_i)
+        dev = torch.device("cuda", dev_i)
+        sync = torch.cuda.synchronize
     dist.init_process_group(backend=args.dist_backend)
     dist.barrier()
-    if rank == 0:
+    if rank == 0 and os.path.exists(leg_flag("side")):
         os.unlink(leg_flag("side"))  # every rank is past side_legs
     comm = ftar.Comm.from_env()
     comm.set_profiling(False)  # kernel events only in the profiled passes (timed_split)
-    g = torch.Generator(device="cuda").manual_seed(1000 + rank)
-    x = torch.rand(args.count, device="cuda", generator=g) * 2 - 1
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.rand(args.count, device=dev, generator=g) * 2 - 1
     y = torch.empty_like(x)
     S = args.count * 4
     nccl = args.dist_backend == "nccl"
+    legs = {}  # per optional leg: status and seconds
 
     def max_over_ranks(vals):
         t = torch.tensor(vals, dtype=torch.float64)
@@ -476,14 +770,18 @@ def multi(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return [v.item() for v in t.cpu()]
 
+    def time_left():
+        # the same on every rank (min over ranks of each rank's budget left)
+        return -max_over_ranks([-(args.budget - (time.monotonic() - T_START))])[0]
+
     def timed(fn, steps=None, warmup=None):
         steps = args.steps if steps is None else steps
         warmup = args.warmup if warmup is None else warmup
         for _ in range(warmup):
             fn()
-        torch.cuda.synchronize()
+        sync()
         dist.barrier()
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
         step0 = kern = syncw = drain = 0.0
         for _ in range(steps):
@@ -493,7 +791,7 @@ def multi(args):
             kern += st.kernel_ms
             syncw += st.sync_wait_s
             drain += st.drain_s
-        torch.cuda.synchronize()
+        sync()
         t1 = time.perf_counter()
         dist.barrier()
         t, k, kall, sw, dr = max_over_ranks([t1 - t0, step0, kern, syncw, drain])
@@ -514,13 +812,18 @@ def multi(args):
         timed_split.breakdown = dict(timed.breakdown, profiled=True)
         return t, k
 
+    class CallFailed(RuntimeError):
+        pass
+
     def raben():
         rc = comm.allreduce_rabenseifner(x, y)
-        assert rc == 0, rc
+        if rc != 0:
+            raise CallFailed(f"allreduce_rabenseifner returned {rc}")
 
     def rd():
         rc = comm.recursive_doubling(x, y)
-        assert rc == 0, rc
+        if rc != 0:
+            raise CallFailed(f"recursive_doubling returned {rc}")
 
     def quick(fn, steps=3, warmup=1):
         return timed(fn, steps, warmup)[0]
@@ -538,13 +841,13 @@ def multi(args):
     # exact in any order.  Each rank regenerates every rank's input from its seed and sums
     # them itself: the expected result needs no collective.  Trials reuse the same buffers
     # (the peers' mappings of our send buffer are reused too).
-    xe = torch.empty(args.count, device="cuda")
+    xe = torch.empty(args.count, device=dev)
     ye = torch.empty_like(xe)
     want = torch.empty_like(xe)
 
     def int_input(out, trial, r, n):
-        ge = torch.Generator(device="cuda").manual_seed(7919 * trial + r)
-        out[:n].copy_(torch.randint(-1024, 1024, (n,), device="cuda", generator=ge, dtype=torch.int32))
+        ge = torch.Generator(device=dev).manual_seed(7919 * trial + r)
+        out[:n].copy_(torch.randint(-1024, 1024, (n,), device=dev, generator=ge, dtype=torch.int32))
 
     def exact_ok(fn, trials=(1, 2), n=None):
         n = args.count if n is None else n
@@ -563,7 +866,8 @@ def multi(args):
     # Transport selection before the timed run: how the node's xGMI links behave under
     # concurrent peer reads decides between the one-hop mesh (power-of-two p without a
     # spare), the 2-hop relay and plain pairwise pulls, so a short comparison (max over
-    # ranks, identical on every rank) picks one.  All three give the same bits.
+    # ranks, identical on every rank) picks one.  All three give the same bits.  A
+    # candidate that fails or is not bit-exact on this node never times the headline.
     selection = None
     pow2 = world & (world - 1) == 0
     if world >= 2 and not args.no_variants:
@@ -574,15 +878,18 @@ def multi(args):
             cands["relay2hop"] = (0, 1)
         cands["direct"] = (0, 0)
         if len(cands) > 1:
-            times, inexact = {}, []
+            times, inexact, failed = {}, [], {}
             for name, (m, r) in cands.items():
                 comm.set_option(ftar.OPT_MESH, m)
                 comm.set_option(ftar.OPT_RELAY, r)
-                # a transport that is not bit-exact on this node never times the headline
-                if max_over_ranks([exact_ok(comm.allreduce_rabenseifner, trials=(0,))])[0]:
-                    inexact.append(name)
-                    continue
-                times[name] = quick(raben)
+                try:
+                    maybe_fail(f"select:{name}")
+                    if max_over_ranks([exact_ok(comm.allreduce_rabenseifner, trials=(0,))])[0]:
+                        inexact.append(name)
+                        continue
+                    times[name] = quick(raben)
+                except Exception as e:
+                    failed[name] = str(e)[-200:]
             if times:
                 chosen = min(times, key=times.get)
                 comm.set_option(ftar.OPT_MESH, cands[chosen][0])
@@ -592,9 +899,9 @@ def multi(args):
                 comm.set_option(ftar.OPT_MESH, defaults[ftar.OPT_MESH])
                 comm.set_option(ftar.OPT_RELAY, defaults[ftar.OPT_RELAY])
             selection = {f"{k}_ms": round(t * 1e3, 4) for k, t in times.items()}
-            selection["chosen"] = chosen
-            selection["inexact"] = inexact
+            selection.update({"chosen": chosen, "inexact": inexact, "failed": failed})
 
+    # ---- the headline: configs[3] ----
     t_rb, k_rb = timed_split(raben)
     step0_bytes = timed.link_bytes
     breakdown = timed_split.breakdown
@@ -603,142 +910,9 @@ def multi(args):
     oneshot = comm.last_stats().mesh_steps == 1  # the mesh's one-launch form (p = 2, small vectors)
     transport = "mesh-oneshot" if oneshot else "mesh" if meshed else "relay2hop" if relayed else "direct"
     chosen_opts = {o: comm.get_option(o) for o in opts}
-    # correctness spot check against torch.distributed's all_reduce on the same inputs
-    # (fp32, different reduction order: |err| <= log2(p) * 2^-24 * sum|x_i|)
-    ref = x.clone() if nccl else x.cpu()
-    dist.all_reduce(ref)
-    raben()
-    err = (y.cpu() - ref.cpu()).abs().max().item()
-    # the reference drivers' case (buffer[i] = rank, int32 SUM): closed-form checksum
-    # sum_i result[i] % 17 = ((p (p-1) / 2) % 17) * count  (analysis/check_fault.py:62-67)
-    xi = torch.full((args.count,), rank, dtype=torch.int32, device="cuda")
-    yi = torch.empty_like(xi)
-    assert comm.allreduce_rabenseifner(xi, yi) == 0
-    cks_raben = int((yi.to(torch.int64) % 17).sum().item())
-    assert comm.recursive_doubling(xi, yi) == 0
-    cks_rd = int((yi.to(torch.int64) % 17).sum().item())
-    cks_want = ((world * (world - 1) // 2) % 17) * args.count
-    del xi, yi
-    # The reference's own data movement, first class: pairwise pulls, step by step, one
-    # link per step, with the step-0 full-vector exchange kept (its tmp redundancy,
-    # raben/rabenseifner.c:206-211) even where no handler can use it.
-    set_opts((0, 0, 0, 1, 0))
-    t_ref, k_ref = timed_split(raben)
-    set_opts([chosen_opts[o] for o in opts])
-    # recursive doubling has no mesh form (it can recover at any p): relay or direct
-    rd_selection = None
-    relay_for_raben = comm.get_option(ftar.OPT_RELAY)
-    if world >= 3 and not args.no_variants:
-        comm.set_option(ftar.OPT_RELAY, 1)
-        t_r = quick(rd)
-        comm.set_option(ftar.OPT_RELAY, 0)
-        t_d = quick(rd)
-        comm.set_option(ftar.OPT_RELAY, 1 if t_r <= t_d else 0)
-        rd_selection = {"relay2hop_ms": round(t_r * 1e3, 4), "direct_ms": round(t_d * 1e3, 4),
-                        "chosen": "relay2hop" if t_r <= t_d else "direct"}
-    t_rd, k_rd = timed_split(rd)
-    comm.set_option(ftar.OPT_RELAY, relay_for_raben)
-    # the same schedules over the other transports
-    transports = {}
-    if not args.no_variants:
-        # mesh: one-hop reduce-scatter + allgather (power-of-two p, no spare); relay2hop:
-        # the step-by-step schedule striped over 2-hop paths; direct: one pull kernel per
-        # step; direct_serial: plus the step-0 copy inline; copy_engine: hipMemcpyAsync of
-        # the partner's window + a local reduce kernel; relay_full_exchange: the relay with
-        # the reference's step-0 full exchange
-        variants = (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
-                    ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
-                    ("relay_full_exchange", (1, 1, 0, 1, 0)))
-        for name, vals in variants:
-            if name == "mesh" and not pow2:
-                continue
-            set_opts(vals)
-            tv, kv = timed_split(raben)
-            lb = timed.link_bytes
-            tv_rd, _ = timed(rd) if name in ("relay2hop", "direct", "copy_engine") else (None, None)
-            transports[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2),
-                                "step0_kernel_ms": round(kv, 4), "step0_link_bytes": lb,
-                                "step0_pull_GBps": round(lb / (kv * 1e-3) / 1e9, 2) if kv > 0 else None}
-            if tv_rd:
-                transports[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
-        set_opts([chosen_opts[o] for o in opts])
-    # Exactness of every transport on this node (helpers above the selection)
-    checks = [("chosen", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, None),
-              ("reference_shape", (0, 0, 0, 1, 0), comm.allreduce_rabenseifner, None),
-              ("rd", [chosen_opts[o] for o in opts], comm.recursive_doubling, None),
-              ("chosen_64KiB", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, 16384)]
-    if not args.no_variants:
-        checks += [(name, vals, comm.allreduce_rabenseifner, None) for name, vals in
-                   (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
-                    ("copy_engine", (0, 1, 1, 0, 0))) if pow2 or name != "mesh"]
-        checks += [("rd_relay", (1, 1, 0, 0, 0), comm.recursive_doubling, None),
-                   ("rd_direct", (0, 1, 0, 0, 0), comm.recursive_doubling, None)]
-    comm.set_profiling(False)
-    fails = []
-    for name, vals, fn, n in checks:
-        set_opts(vals)
-        if name == "rd" and rd_selection:  # the transport the RD timing chose
-            comm.set_option(ftar.OPT_RELAY, int(rd_selection["chosen"] == "relay2hop"))
-        fails.append(exact_ok(fn, n=n))
-    set_opts([chosen_opts[o] for o in opts])
-    comm.set_profiling(True)
-    fails = max_over_ranks(fails)
-    exact = {"inputs": "integer-valued float32 in [-1024, 1024), new per trial, 2 trials per transport; expected "
-                       "sum regenerated on every rank (exact in any order)",
-             "all_exact": all(f == 0 for f in fails)}
-    exact.update({name: f == 0 for (name, _, _, _), f in zip(checks, fails)})
-    del xe, ye, want
-    # Per-call time over message sizes (max over ranks), 4 B .. 256 MiB, with the chosen
-    # transport, next to RCCL's all_reduce on the same sizes: the FT/vendor curve of the
-    # reference's compare campaign (slurm/test_compare.slurm:27-50, check_compare.py),
-    # plus the fixed cost per call and the one-shot threshold (FTAR_ONESHOT_MAX)
-    sizes = {}
-    if not args.no_variants:
-        comm.set_profiling(False)  # no kernel events: the plain per-call cost
-        oneshot_max = comm.get_option(ftar.OPT_ONESHOT_MAX)
-        z = x.clone() if nccl else None
-        n = 1
-        while n <= args.count:
-            steps, warm = (20, 3) if n <= (1 << 22) else (5, 2)
-            row = {"bytes": 4 * n}
-            for name, fn, extra in (("raben", comm.allreduce_rabenseifner, None),
-                                    ("raben_no_oneshot", comm.allreduce_rabenseifner, 0),
-                                    ("rd", comm.recursive_doubling, None)):
-                if extra is not None:
-                    if not (pow2 and comm.get_option(ftar.OPT_MESH) and oneshot_max > 0) or \
-                            (world > 2 and 4 * n > oneshot_max):
-                        continue
-                    comm.set_option(ftar.OPT_ONESHOT_MAX, extra)
-
-                def call(fn=fn, n=n):
-                    rc = fn(x, y, count=n)
-                    assert rc == 0, rc
-
-                row[name + "_us"] = round(quick(call, steps=steps, warmup=warm) * 1e6, 2)
-                comm.set_option(ftar.OPT_ONESHOT_MAX, oneshot_max)
-            if z is not None:
-                zn = z[:n]
-                row["rccl_us"] = round(quick(lambda: dist.all_reduce(zn), steps=steps, warmup=warm) * 1e6, 2)
-                row["raben_over_rccl"] = round(row["raben_us"] / row["rccl_us"], 3)
-            sizes[str(4 * n)] = row
-            n *= 2
-        comm.set_profiling(True)
-    # end-to-end with host buffers: pinned H2D + device Allreduce + D2H (never the value)
-    xh = x.cpu().pin_memory()
-    yh = torch.empty_like(xh).pin_memory()
-
-    def raben_host():
-        rc = comm.allreduce_rabenseifner_host(xh, yh)
-        assert rc == 0, rc
-
-    t_e2e, _ = timed(raben_host, 3, 1)
-    t_nc = None
-    if nccl:
-        zz = x.clone()
-        t_nc, _ = timed(lambda: dist.all_reduce(zz))
 
     L = world.bit_length() - 1
-    r = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
+    r_core = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
     # Link bytes per rank per direction.  The reference's FT Raben moves
     # (2.5 - 2^(1-L)) S: its step 0 exchanges the full vector, half of it only as
     # recovery data.  At power-of-two p no handler can use that half (they all abort
@@ -747,46 +921,44 @@ def multi(args):
     # over r-1 links); a direct step moves it over one link.
     ft_bytes = (2.5 - 2.0 ** (1 - L)) * S
     classic = 2 * (1 - 2.0 ** -L) * S
-    keep = world != r or comm.get_option(ftar.OPT_REDUNDANCY) != 0
+    keep = world != r_core or comm.get_option(ftar.OPT_REDUNDANCY) != 0
     sched_bytes = ft_bytes if keep else classic
     if oneshot:
-        # every peer's whole vector over its own link: S per link (= 2 S / p at p = 2)
-        t_roof = S / (XGMI_LINK_GBS * 1e9)
+        per_link = float(S)  # every peer's whole vector over its own link (= 2 S / p at p = 2)
     elif meshed:
-        # one hop over p - 1 links: S/p per link for each of reduce-scatter and allgather
-        t_roof = 2.0 * S / world / (XGMI_LINK_GBS * 1e9)
+        per_link = 2.0 * S / world  # one hop over p - 1 links: S/p each for RS and AG
     elif relayed:
-        t_roof = 2.0 / r * sched_bytes / (XGMI_LINK_GBS * 1e9)
+        per_link = 2.0 / r_core * sched_bytes
     elif comm.get_option(ftar.OPT_OVERLAP) != 0:
-        t_roof = classic / (XGMI_LINK_GBS * 1e9)
+        per_link = classic
     else:
-        t_roof = sched_bytes / (XGMI_LINK_GBS * 1e9)
-    t_survey = ft_bytes / (XGMI_LINK_GBS * 1e9)  # the FT schedule on one link per step
-    links = (world - 1) if meshed else (r - 1) if relayed else 1
-    peak = links * XGMI_LINK_GBS
-    achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernels' pulled bytes
+        per_link = sched_bytes
+    links = (world - 1) if meshed else (r_core - 1) if relayed else 1
 
-    def frac(x):
+    def frac(v):
         # a one-GPU rehearsal has no xGMI link in the path (every "peer" read is local
         # HBM shared by all ranks): link-roofline fractions would mix yardsticks
-        return None if rehearsal else round(x, 4)
-    # Link calibration ("B_link = the calibrated single-link unidirectional
-    # GB/s with both directions loaded"): the direct transport's RS step 0 is one kernel
-    # per rank pulling the partner's half over ONE link while the partner pulls ours, so
-    # its pulled bytes / its duration is that figure, measured in this job.
-    link_cal = None
-    dcal = transports.get("direct", {})
-    probe = (xgmi or {}).get("patterns", {}).get("pull1_bidir", {})
-    if dcal.get("step0_pull_GBps") or probe.get("GBps_per_link"):
-        # the probe's plain copy over one link, both ways, where it ran on the node;
-        # otherwise the direct transport's step-0 pull
-        b = probe.get("GBps_per_link") if probe.get("ok") and probe.get("GBps_per_link") else dcal.get("step0_pull_GBps")
-        link_cal = {"single_link_GBps": b, "spec_GBps": XGMI_LINK_GBS, "frac_of_spec": frac(b / XGMI_LINK_GBS),
-                    "source": "xgmi_probe pull1_bidir" if b == probe.get("GBps_per_link") else "direct step 0",
-                    "direct_step0": {"kernel": "direct transport, Raben RS step 0: pull the partner's half + reduce, "
-                                               "both directions loaded", "bytes": dcal.get("step0_link_bytes"),
-                                     "kernel_ms": dcal.get("step0_kernel_ms"),
-                                     "pull_GBps": dcal.get("step0_pull_GBps")}}
+        return None if rehearsal or v is None else round(v, 4)
+
+    def link_cal_from(transports):
+        """SURVEY.md 8d's B_link measured in this job: the probe's plain copy over one link,
+        both directions loaded (pull1_bidir), where it ran on the node; otherwise the
+        direct transport's RS step 0 (one kernel per rank pulling the partner's half over
+        ONE link while the partner pulls ours)."""
+        dcal = transports.get("direct", {})
+        probe = (xgmi or {}).get("patterns", {}).get("pull1_bidir", {})
+        use_probe = bool(probe.get("ok") and probe.get("GBps_per_link")) and not rehearsal
+        b = probe.get("GBps_per_link") if use_probe else dcal.get("step0_pull_GBps")
+        if not b:
+            return None
+        return {"single_link_GBps": b, "nominal_GBps_assumed": XGMI_LINK_GBS, "survey_GBps_assumed": SURVEY_LINK_GBS,
+                "frac_of_nominal": frac(b / XGMI_LINK_GBS),
+                "source": "xgmi_probe pull1_bidir" if use_probe else "direct step 0",
+                "rehearsal_note": "one GPU: the 'link' is the shared HBM, not a calibration" if rehearsal else None,
+                "direct_step0": {"kernel": "direct transport, Raben RS step 0: pull the partner's half + reduce, "
+                                           "both directions loaded", "bytes": dcal.get("step0_link_bytes"),
+                                 "kernel_ms": dcal.get("step0_kernel_ms"), "pull_GBps": dcal.get("step0_pull_GBps")}}
+
     schedule = {
         "mesh-oneshot": "Rabenseifner, one-shot mesh: every block in its owner's reduction tree in one launch "
                         "(power-of-two p, no spare)",
@@ -796,12 +968,20 @@ def multi(args):
                      "relays",
         "direct": "Rabenseifner, step by step (recursive halving + doubling), one pairwise pull per step",
     }[transport]
-    if rank == 0:
-        out = {
+
+    def build_line(transports, t_ref, k_ref):
+        cal = link_cal_from(transports)
+        b_link = cal["single_link_GBps"] if cal and not rehearsal else None
+        b_price = b_link or XGMI_LINK_GBS
+        t_roof = per_link / (b_price * 1e9)
+        t_survey = ft_bytes / (b_price * 1e9)  # the FT schedule on one link per step
+        achieved = step0_bytes / (k_rb * 1e-3) / 1e9 if k_rb > 0 else None  # RS step-0 kernels' pulled bytes
+        peak = links * b_price
+        line = {
             "metric": METRIC, "value": round(world * S / t_rb / 1e9, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_rb * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic uniform[-1,1), HBM-resident",
+            "data": "synthetic uniform[-1,1), HBM-resident" + (" (CPU TEST: host-sim library)" if cpu_mode else ""),
             "config": {"workload": f"configs[3]: fault-tolerant Rabenseifner Allreduce, 256 MiB float32 SUM per "
                                    f"rank, one rank per MI355X -- {schedule}",
                        "schedule": schedule, "transport": transport,
@@ -814,25 +994,23 @@ def multi(args):
             # the headline call of the profiled pass split into device time (all kernels /
             # the dominant one) and the host's waits (agree + barrier rounds, stream drains)
             "call_breakdown": breakdown,
-            "reference_shape": {
-                "schedule": "Rabenseifner step by step, pairwise pulls (one xGMI link per step), step-0 full-vector "
-                            "exchange kept (raben/rabenseifner.c:206-211)",
-                "value": round(world * S / t_ref / 1e9, 2), "ms_per_step": round(t_ref * 1e3, 4),
-                "algbw_GBps": round(S / t_ref / 1e9, 2), "step0_kernel_ms": round(k_ref, 4),
-                "survey_ft_roofline_ms": round(t_survey * 1e3, 3),
-                "frac_of_survey_roofline": frac(t_survey / t_ref)},
-            "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "link_GBps": XGMI_LINK_GBS,
-                                       "links_per_step": links, "t_roof_ms": round(t_roof * 1e3, 3),
-                                       "frac": frac(t_roof / t_rb),
-                                       # the same roofline priced at the calibrated link rate
-                                       "frac_calibrated_link": frac(t_roof * XGMI_LINK_GBS
-                                                                    / link_cal["single_link_GBps"] / t_rb)
-                                       if link_cal else None},
-            "link_calibration": link_cal,
+            "north_star": north_star_block(world, S, t_rb, transport, b_link, links, per_link, t_ref, rehearsal),
+            "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "bytes_per_link": per_link,
+                                       "links_per_step": links,
+                                       "link_GBps": b_price,
+                                       "link_basis": "calibrated" if b_link else "nominal 76.8 GB/s per direction "
+                                                                                 "(assumption)",
+                                       "t_roof_ms": round(t_roof * 1e3, 4), "frac": frac(t_roof / t_rb),
+                                       "frac_nominal_76.8": frac(per_link / (XGMI_LINK_GBS * 1e9) / t_rb),
+                                       "frac_survey_153.6": frac(per_link / (SURVEY_LINK_GBS * 1e9) / t_rb)},
+            "link_calibration": cal,
             "xgmi_probe": xgmi,
             "roofline": {"bound": "xgmi", "achieved": round(achieved, 1) if achieved else None,
-                         "peak": peak, "unit": "GB/s",
+                         "peak": round(peak, 2), "unit": "GB/s",
+                         "peak_basis": f"{links} link(s) x " + (f"{b_link} GB/s calibrated" if b_link else
+                                                               f"{XGMI_LINK_GBS} GB/s nominal (assumption)"),
                          "frac": frac(achieved / peak) if achieved else None,
+                         "frac_nominal_76.8": frac(achieved / (links * XGMI_LINK_GBS)) if achieved else None,
                          "rehearsal": rehearsal,
                          # HBM bytes per launch from PMC exist for the one-GPU rehearsal only
                          # (every peer on this device); on the node the peer reads hit the
@@ -848,22 +1026,246 @@ def multi(args):
                                     else "Raben RS step 0, both relay phases (stripes pulled over r-1 links)" if relayed
                                     else "Raben RS step 0 reduce half (pull partner's half, reduce into W)"),
                          "algorithmic_bytes_per_launch": step0_bytes, "kernel_ms": round(k_rb, 4)},
-            "e2e_host_buffers": {"ms_per_step": round(t_e2e * 1e3, 3), "algbw_GBps": round(S / t_e2e / 1e9, 2)},
-            "rd": {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
-                   "value": round(world * S / t_rd / 1e9, 2),
-                   "step0_kernel_ms": round(k_rd, 4), "transport_selection": rd_selection},
-            "rccl_allreduce": ({"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2),
-                                "value": round(world * S / t_nc / 1e9, 2)} if t_nc else None),
             "transport_selection": selection,
-            "transports": transports,
-            "size_sweep_us": sizes,
-            "max_abs_err_vs_rccl": err,
-            "int32_rank_checksum_ok": {"raben": cks_raben == cks_want, "rd": cks_rd == cks_want},
-            "exact_on_node": exact,
-            "c5_single_kill": c5,
             "cpu_baseline": cpu,
+            "side_legs": side_info,
         }
-        print(json.dumps(out), flush=True)
+        if t_ref:
+            line["reference_shape"] = {
+                "schedule": "Rabenseifner step by step, pairwise pulls (one xGMI link per step), step-0 full-vector "
+                            "exchange kept (raben/rabenseifner.c:206-211)",
+                "value": round(world * S / t_ref / 1e9, 2), "ms_per_step": round(t_ref * 1e3, 4),
+                "algbw_GBps": round(S / t_ref / 1e9, 2), "step0_kernel_ms": round(k_ref, 4),
+                "survey_ft_roofline_ms": round(t_survey * 1e3, 4),
+                "frac_of_survey_roofline": frac(t_survey / t_ref),
+                "frac_of_survey_roofline_nominal_76.8": frac(ft_bytes / (XGMI_LINK_GBS * 1e9) / t_ref),
+                "frac_of_survey_roofline_survey_153.6": frac(ft_bytes / (SURVEY_LINK_GBS * 1e9) / t_ref)}
+        return line
+
+    line = build_line({}, None, 0.0)
+    dog.line = line
+    if rank == 0:
+        print(json.dumps(dict(line, line="headline")), flush=True)
+
+    # ---- optional legs: each runs only while the budget has room, records its own fate ----
+    def opt_leg(name, est_s, fn):
+        t0 = time.monotonic()
+        if time_left() < est_s:
+            legs[name] = {"status": "skipped", "reason": f"budget: needs ~{est_s:.0f} s"}
+            return None
+        try:
+            maybe_fail(name)
+            if test_hook("hang", name):  # TEST-ONLY: an in-process leg that never returns
+                time.sleep(3600)
+            r = fn()
+            legs[name] = {"status": "ok", "s": round(time.monotonic() - t0, 2)}
+            return r
+        except Exception as e:  # uniform on every rank for the failures a leg raises itself
+            legs[name] = {"status": "error", "s": round(time.monotonic() - t0, 2), "error": str(e)[-400:]}
+            return None
+
+    def checks_leg():
+        # correctness spot check against torch.distributed's all_reduce on the same inputs
+        # (fp32, different reduction order: |err| <= log2(p) * 2^-24 * sum|x_i|)
+        ref = x.clone() if nccl or cpu_mode else x.cpu()
+        dist.all_reduce(ref)
+        raben()
+        err = (y.cpu() - ref.cpu()).abs().max().item()
+        # the reference drivers' case (buffer[i] = rank, int32 SUM): closed-form checksum
+        # sum_i result[i] % 17 = ((p (p-1) / 2) % 17) * count  (analysis/check_fault.py:62-67)
+        xi = torch.full((args.count,), rank, dtype=torch.int32, device=dev)
+        yi = torch.empty_like(xi)
+        if comm.allreduce_rabenseifner(xi, yi) != 0:
+            raise CallFailed("int32 Rabenseifner failed")
+        cks_raben = int((yi.to(torch.int64) % 17).sum().item())
+        if comm.recursive_doubling(xi, yi) != 0:
+            raise CallFailed("int32 recursive doubling failed")
+        cks_rd = int((yi.to(torch.int64) % 17).sum().item())
+        cks_want = ((world * (world - 1) // 2) % 17) * args.count
+        return err, {"raben": cks_raben == cks_want, "rd": cks_rd == cks_want}
+
+    def exact_leg():
+        # Exactness of every transport on this node (helpers above the selection)
+        checks = [("chosen", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, None),
+                  ("reference_shape", (0, 0, 0, 1, 0), comm.allreduce_rabenseifner, None),
+                  ("rd", [chosen_opts[o] for o in opts], comm.recursive_doubling, None),
+                  ("chosen_64KiB", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, 16384)]
+        if not args.no_variants:
+            checks += [(name, vals, comm.allreduce_rabenseifner, None) for name, vals in
+                       (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
+                        ("copy_engine", (0, 1, 1, 0, 0))) if pow2 or name != "mesh"]
+            checks += [("rd_relay", (1, 1, 0, 0, 0), comm.recursive_doubling, None),
+                       ("rd_direct", (0, 1, 0, 0, 0), comm.recursive_doubling, None)]
+        comm.set_profiling(False)
+        fails = []
+        try:
+            for name, vals, fn, n in checks:
+                set_opts(vals)
+                if name == "rd" and rd_selection:  # the transport the RD timing chose
+                    comm.set_option(ftar.OPT_RELAY, int(rd_selection["chosen"] == "relay2hop"))
+                fails.append(exact_ok(fn, n=n))
+        finally:
+            set_opts([chosen_opts[o] for o in opts])
+            comm.set_profiling(True)
+        fails = max_over_ranks(fails)
+        exact = {"inputs": "integer-valued float32 in [-1024, 1024), new per trial, 2 trials per transport; "
+                           "expected sum regenerated on every rank (exact in any order)",
+                 "all_exact": all(f == 0 for f in fails)}
+        exact.update({name: f == 0 for (name, _, _, _), f in zip(checks, fails)})
+        return exact
+
+    def ref_shape_leg():
+        # The reference's own data movement, first class: pairwise pulls, step by step, one
+        # link per step, with the step-0 full-vector exchange kept (its tmp redundancy,
+        # raben/rabenseifner.c:206-211) even where no handler can use it.
+        set_opts((0, 0, 0, 1, 0))
+        try:
+            return timed_split(raben)
+        finally:
+            set_opts([chosen_opts[o] for o in opts])
+
+    rd_selection = None
+
+    def rd_leg():
+        # recursive doubling has no mesh form (it can recover at any p): relay or direct
+        nonlocal rd_selection
+        relay_for_raben = comm.get_option(ftar.OPT_RELAY)
+        try:
+            if world >= 3 and not args.no_variants:
+                comm.set_option(ftar.OPT_RELAY, 1)
+                t_r = quick(rd)
+                comm.set_option(ftar.OPT_RELAY, 0)
+                t_d = quick(rd)
+                comm.set_option(ftar.OPT_RELAY, 1 if t_r <= t_d else 0)
+                rd_selection = {"relay2hop_ms": round(t_r * 1e3, 4), "direct_ms": round(t_d * 1e3, 4),
+                                "chosen": "relay2hop" if t_r <= t_d else "direct"}
+            t_rd, k_rd = timed_split(rd)
+        finally:
+            comm.set_option(ftar.OPT_RELAY, relay_for_raben)
+        return {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
+                "value": round(world * S / t_rd / 1e9, 2), "step0_kernel_ms": round(k_rd, 4),
+                "transport_selection": rd_selection}
+
+    def rccl_leg():
+        zz = x.clone()
+        t_nc, _ = timed(lambda: dist.all_reduce(zz))
+        return {"ms_per_step": round(t_nc * 1e3, 4), "algbw_GBps": round(S / t_nc / 1e9, 2),
+                "value": round(world * S / t_nc / 1e9, 2)}
+
+    def transports_leg():
+        # mesh: one-hop reduce-scatter + allgather (power-of-two p, no spare); relay2hop:
+        # the step-by-step schedule striped over 2-hop paths; direct: one pull kernel per
+        # step; direct_serial: plus the step-0 copy inline; copy_engine: hipMemcpyAsync of
+        # the partner's window + a local reduce kernel; relay_full_exchange: the relay with
+        # the reference's step-0 full exchange.  Each variant records its own failure.
+        out = {}
+        variants = (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
+                    ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
+                    ("relay_full_exchange", (1, 1, 0, 1, 0)))
+        try:
+            for name, vals in variants:
+                if name == "mesh" and not pow2:
+                    continue
+                if time_left() < 10:
+                    out[name] = {"skipped": "budget"}
+                    continue
+                try:
+                    maybe_fail(f"transports:{name}")
+                    set_opts(vals)
+                    tv, kv = timed_split(raben)
+                    lb = timed.link_bytes
+                    tv_rd = timed(rd)[0] if name in ("relay2hop", "direct", "copy_engine") else None
+                    out[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2),
+                                 "step0_kernel_ms": round(kv, 4), "step0_link_bytes": lb,
+                                 "step0_pull_GBps": round(lb / (kv * 1e-3) / 1e9, 2) if kv > 0 else None}
+                    if tv_rd:
+                        out[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
+                except Exception as e:
+                    out[name] = {"error": str(e)[-300:]}
+        finally:
+            set_opts([chosen_opts[o] for o in opts])
+        return out
+
+    def sweep_leg():
+        # Per-call time over message sizes (max over ranks), 4 B .. 256 MiB, with the chosen
+        # transport, next to RCCL's all_reduce on the same sizes: the FT/vendor curve of the
+        # reference's compare campaign (slurm/test_compare.slurm:27-50, check_compare.py),
+        # plus the fixed cost per call and the one-shot threshold (FTAR_ONESHOT_MAX)
+        sizes = {}
+        comm.set_profiling(False)  # no kernel events: the plain per-call cost
+        oneshot_max = comm.get_option(ftar.OPT_ONESHOT_MAX)
+        z = x.clone() if nccl else None
+        n = 1
+        try:
+            while n <= args.count:
+                if time_left() < 15:
+                    sizes["truncated_at_bytes"] = 4 * n
+                    break
+                steps, warm = (20, 3) if n <= (1 << 22) else (5, 2)
+                row = {"bytes": 4 * n}
+                for name, fn, extra in (("raben", comm.allreduce_rabenseifner, None),
+                                        ("raben_no_oneshot", comm.allreduce_rabenseifner, 0),
+                                        ("rd", comm.recursive_doubling, None)):
+                    if extra is not None:
+                        if not (pow2 and comm.get_option(ftar.OPT_MESH) and oneshot_max > 0) or \
+                                (world > 2 and 4 * n > oneshot_max):
+                            continue
+                        comm.set_option(ftar.OPT_ONESHOT_MAX, extra)
+
+                    def call(fn=fn, n=n):
+                        if fn(x, y, count=n) != 0:
+                            raise CallFailed(f"size sweep call of {4 * n} B failed")
+
+                    try:
+                        row[name + "_us"] = round(quick(call, steps=steps, warmup=warm) * 1e6, 2)
+                    finally:
+                        comm.set_option(ftar.OPT_ONESHOT_MAX, oneshot_max)
+                if z is not None:
+                    zn = z[:n]
+                    row["rccl_us"] = round(quick(lambda: dist.all_reduce(zn), steps=steps, warmup=warm) * 1e6, 2)
+                    row["raben_over_rccl"] = round(row["raben_us"] / row["rccl_us"], 3)
+                sizes[str(4 * n)] = row
+                n *= 2
+        finally:
+            comm.set_profiling(True)
+        return sizes
+
+    def e2e_leg():
+        # end-to-end with host buffers: pinned H2D + device Allreduce + D2H (never the value)
+        xh = x.cpu() if cpu_mode else x.cpu().pin_memory()
+        yh = torch.empty_like(xh) if cpu_mode else torch.empty_like(xh).pin_memory()
+
+        def raben_host():
+            if comm.allreduce_rabenseifner_host(xh, yh) != 0:
+                raise CallFailed("host-buffer Rabenseifner failed")
+
+        t_e2e, _ = timed(raben_host, 3, 1)
+        return {"ms_per_step": round(t_e2e * 1e3, 3), "algbw_GBps": round(S / t_e2e / 1e9, 2)}
+
+    final = {}
+    ck = opt_leg("checks", 10, checks_leg)
+    if ck:
+        final["max_abs_err_vs_rccl"], final["int32_rank_checksum_ok"] = ck
+    rs = opt_leg("reference_shape", 15, ref_shape_leg)
+    t_ref, k_ref = rs if rs else (None, 0.0)
+    final["rd"] = opt_leg("rd", 15, rd_leg)
+    final["exact_on_node"] = opt_leg("exact_on_node", 30, exact_leg)
+    final["rccl_allreduce"] = opt_leg("rccl_allreduce", 10, rccl_leg) if nccl else None
+    transports = {} if args.no_variants else (opt_leg("transports", 40, transports_leg) or {})
+    final["transports"] = transports
+    final["size_sweep_us"] = {} if args.no_variants else opt_leg("size_sweep", 40, sweep_leg)
+    final["e2e_host_buffers"] = opt_leg("e2e_host_buffers", 20, e2e_leg)
+    del xe, ye, want
+
+    line = build_line(transports, t_ref, k_ref)
+    line.update(final)
+    line["c5_single_kill"] = c5
+    line["legs"] = legs
+    line["job_s"] = round(time.monotonic() - T_START, 1)
+    dog.line = line
+    if rank == 0:
+        print(json.dumps(dict(line, line="final")), flush=True)
+    dog.done.set()
     comm.finalize()
     dist.destroy_process_group()
 
@@ -883,6 +1285,12 @@ def main():
                     help="N=1 kernel time: events around the timed region, or around every launch")
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the transport comparison and size sweep")
     ap.add_argument("--dist-backend", default="nccl", help="torch.distributed backend for barrier/timing")
+    ap.add_argument("--side-budget", type=float, default=150.0,
+                    help="N>1: seconds for all side legs together (CPU baseline, fabric probe, configs[4] jobs)")
+    ap.add_argument("--budget", type=float, default=480.0,
+                    help="N>1: seconds for the whole job; optional legs run only while it has room")
+    ap.add_argument("--c5-draws", type=int, default=10, help="N>1: random-kill draws of the configs[4] campaign")
+    ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu", help=argparse.SUPPRESS)
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:

@@ -51,6 +51,21 @@ class Kill(ctypes.Structure):
 
 
 _lib = None
+_test_lib_path = None
+
+
+def use_test_library(path: str):
+    """TEST-ONLY: bind the host-memory build of the same C sources (tests/hostsim/_build/
+    libftar_hostsim.so) instead of lib/libftar.so, so bench.py's N > 1 control flow can be
+    exercised on a CPU-only machine (tests/test_bench_logic.py, `bench.py --device cpu`
+    under FTAR_BENCH_CPU_TEST=1).  Refuses any other library, and refuses once the product
+    library is bound; the product path and the GPU tests never call it."""
+    global _test_lib_path
+    if _lib is not None:
+        raise FtarError("the product library is already bound")
+    if os.path.basename(path) != "libftar_hostsim.so" or not os.path.exists(path):
+        raise FtarError(f"{path} is not the host-sim test library")
+    _test_lib_path = path
 
 
 def build(jobs: int = 8) -> str:
@@ -63,9 +78,10 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise FtarError(f"{LIB_PATH} is not built: run `make -C {HERE}` (the HIP path has no fallback)")
-    L = ctypes.CDLL(LIB_PATH)
+    path = _test_lib_path or LIB_PATH
+    if not os.path.exists(path):
+        raise FtarError(f"{path} is not built: run `make -C {HERE}` (the HIP path has no fallback)")
+    L = ctypes.CDLL(path)
     vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
     pp = ctypes.POINTER(vp)
     sig = {
@@ -115,7 +131,8 @@ def _ptr(x):
     pinned host tensor (the kernels read and write it in place over PCIe; include/ftar.h)."""
     if isinstance(x, int):
         return x
-    if not x.is_contiguous() or not (x.is_cuda or x.is_pinned()):
+    # (host-sim test library: its "device" memory is host memory)
+    if not x.is_contiguous() or not (x.is_cuda or _test_lib_path is not None or x.is_pinned()):
         raise FtarError("buffers must be contiguous device tensors or pinned host tensors")
     return x.data_ptr()
 

@@ -13,6 +13,10 @@ Rules restated from the reference:
   SEGFAULT           "Segmentation fault" or "(core dumped)" in the test log
   KILLED             N - number of distinct ranks that printed "Hello"
   TIME               the last "Time:" printed by a rank, else the `time` real value
+Beside the row, <log.csv>.victims gets N;KILLED;VICTIMS;MID EXCHANGE from the launcher's
+post mortem (ftrun prints, for every rank killed by a signal, whether a kernel reading
+peers' HBM was in flight): the GPU exchange takes milliseconds, so whether a random kill
+met data movement is recorded rather than assumed.
 """
 import csv
 import os
@@ -38,9 +42,12 @@ def parse_real(token):
 
 
 def read_test_log(path):
-    info = {"segfault": False, "abort": False, "real": None}
+    info = {"segfault": False, "abort": False, "real": None, "victims": []}
     with open(path) as f:
         for raw in f:
+            m = re.match(r"ftrun: rank (\d+) \(pid \d+\) killed by signal \d+ (.*)", raw.strip())
+            if m:  # the launcher's post mortem of a killed rank (not in the reference)
+                info["victims"].append((int(m.group(1)), m.group(2).startswith("mid-exchange")))
             if "Segmentation fault" in raw or "(core dumped)" in raw:
                 info["segfault"] = True
             tok = raw.split()
@@ -106,6 +113,16 @@ def main(argv):
         if new:
             w.writerow(HEADER)
         w.writerow(row)
+    # Row-side log (the reference's CSV grammar stays untouched): which ranks the launcher
+    # saw killed by a signal and whether each died mid-exchange, one line per CSV row.
+    side = log_file + ".victims"
+    new = not os.path.exists(side)
+    with open(side, "a", newline="") as f:
+        w = csv.writer(f, delimiter=";")
+        if new:
+            w.writerow(["N", "KILLED", "VICTIMS", "MID EXCHANGE"])
+        v = info["victims"]
+        w.writerow([n, killed, " ".join(str(r) for r, _ in v), any(mid for _, mid in v) if v else ""])
 
 
 if __name__ == "__main__":

@@ -113,6 +113,16 @@ void ftar_maybe_die(ftar_comm *c, int phase, int step, int point)
             fprintf(stderr, "ftar: rank %d dies mid-exchange (phase %d step %d): own kernel %s, %d peers launched\n",
                     c->wrank, phase, step, busy ? "in flight" : "complete", peers);
         }
+        if (getenv("FTAR_KILL_WITHDRAW")) {
+            /* TEST-ONLY: the victim's input is gone with it (as after the loss of its device):
+             * its workspace generation moves on and its published sbuf is withdrawn, so no
+             * peer may read either (ftar_dead_input) */
+            ftar_slot *me = &c->job.shm->slot[c->wrank];
+            atomic_fetch_add(&me->ws_gen, 1);
+            me->uid = 0;
+            me->useq = 0;
+            fprintf(stderr, "ftar: rank %d withdraws its input before dying\n", c->wrank);
+        }
         if (c->verbose) fprintf(stderr, "ftar: rank %d dies at phase %d step %d point %d\n", c->wrank, phase, step, point);
         fflush(stdout);
         fflush(stderr);
@@ -314,6 +324,7 @@ void ftar_resolve_inputs(ftar_comm *c)
         for (int i = 0; i < c->size; i++) any |= c->job.shm->slot[c->order[i]].ufail == (uint64_t)c->ncalls;
         if (any) {
             c->export_user = 0;
+            me->uid = 0; /* this call's input is the staged IN from here on (ftar_dead_input) */
             if (c->in_alias) { /* stage the whole vector: what every schedule reads from IN */
                 fdev_seg s = {FDEV_COPY, 0, c->ws[WS_IN], c->in_alias, NULL, c->in_bytes / 4, NULL};
                 ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL);
@@ -327,6 +338,16 @@ void ftar_resolve_inputs(ftar_comm *c)
         int w = c->order[i];
         c->last_uid[w] = c->export_user ? published_id(c, w) : 0;
     }
+}
+
+const void *ftar_dead_input(ftar_comm *c, int w, size_t bytes)
+{
+    ftar_slot *s = &c->job.shm->slot[w];
+    if (s->useq != (uint64_t)c->ncalls) return NULL; /* not this call's input */
+    if (c->peer_in[w]) return s->uid ? c->peer_in[w] : NULL; /* its sbuf, exported for this call */
+    if (s->uid || !c->peer[w][WS_IN]) return NULL;
+    if (c->peer_gen[w] != atomic_load(&s->ws_gen) || c->peer_bytes[w] < bytes) return NULL;
+    return c->peer[w][WS_IN];
 }
 
 void ftar_inputs_done(ftar_comm *c)
@@ -345,6 +366,7 @@ int ftar_finalize(ftar_comm *c)
     for (int b = 0; b < FTAR_NBUF; b++) fdev_free(c->dev, c->ws[b]);
     fdev_free(c->dev, c->hsend);
     fdev_free(c->dev, c->hrecv);
+    fdev_free(c->dev, c->pad);
     ftar_ctrl_leave(&c->job);
     fdev_close(c->dev);
     ftar_ctrl_detach(&c->job);
@@ -435,12 +457,32 @@ int ftar_barrier(ftar_comm *c)
 
 /* ---- synchronisation ------------------------------------------------------ */
 
+/* FTAR_LOOP_SECONDS (the harness's stretch of the schedule, run/run_mpi.sh): the reference's
+ * CPU exchanges take seconds, so its random kills land in data movement; a GPU step takes
+ * milliseconds.  Instead of idling, the step re-pulls its last peer window (up to
+ * FTAR_PAD_BYTES of it) into local scratch again and again until its share of the stretch
+ * is used up: a kill then meets pull kernels in flight.  The re-pulls are idempotent reads
+ * of a window that is stable until the next barrier (or of a dead peer's still-mapped
+ * memory) into a buffer nothing else reads, so results and decisions do not change. */
 uint64_t ftar_step_sync(ftar_comm *c, int nsteps)
 {
     if (c->loop_seconds > 0 && nsteps > 0) { /* busy (R state), like a rank inside its exchange */
         double t0 = now_s(), d = c->loop_seconds / nsteps;
-        while (now_s() - t0 < d) ftar_ctrl_poll(&c->job);
+        if (c->pad_src && !c->pad && fdev_alloc_plain(c->dev, FTAR_PAD_BYTES, &c->pad)) c->pad = NULL;
+        while (now_s() - t0 < d) {
+            if (c->pad_src && c->pad) {
+                size_t n = c->pad_bytes < FTAR_PAD_BYTES ? c->pad_bytes : FTAR_PAD_BYTES;
+                fdev_seg s = {FDEV_COPY, FDEV_REMOTE_X, c->pad, c->pad_src, NULL, n / 4, NULL};
+                const void *src = c->pad_src;
+                if (n / 4 == 0 || ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL)) break;
+                ftar_drain(c);
+                c->pad_src = src; /* ftar_run noted it again; keep it for the next round */
+            } else {
+                ftar_ctrl_poll(&c->job);
+            }
+        }
     }
+    c->pad_src = NULL; /* the next step re-pulls what it reads itself */
     return ftar_sync(c);
 }
 
@@ -493,10 +535,35 @@ void ftar_launched(ftar_comm *c, int phase, int step)
 
 void ftar_exchange_done(ftar_comm *c) { ftar_ctrl_done(&c->job); }
 
+void ftar_note_launch(ftar_comm *c, const void *remote, size_t bytes)
+{
+    _Atomic int *w = &c->job.shm->slot[c->wrank].inflight;
+    if (remote) {
+        atomic_store_explicit(w, FTAR_INFLIGHT_PULL, memory_order_release);
+        c->pad_src = remote;
+        c->pad_bytes = bytes;
+    } else if (atomic_load_explicit(w, memory_order_relaxed) == 0) {
+        atomic_store_explicit(w, FTAR_INFLIGHT_LOCAL, memory_order_release);
+    }
+}
+
+static void note_segs(ftar_comm *c, int dtype, const fdev_seg *segs, int nseg)
+{
+    const void *remote = NULL;
+    size_t bytes = 0;
+    for (int i = 0; i < nseg && !remote; i++) {
+        if (segs[i].remote & FDEV_REMOTE_X) remote = segs[i].x;
+        else if (segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) remote = segs[i].y;
+        bytes = segs[i].n * ftar_esize(dtype);
+    }
+    ftar_note_launch(c, remote, bytes);
+}
+
 int ftar_drain(ftar_comm *c)
 {
     double t0 = now_s();
     int rc = fdev_sync(c->dev, ftar_ctrl_poll, &c->job);
+    if (!rc) atomic_store_explicit(&c->job.shm->slot[c->wrank].inflight, 0, memory_order_release);
     c->stats.drain_s += now_s() - t0;
     if (rc) {
         fprintf(stderr, "ftar: rank %d: device error: %s\n", c->wrank, fdev_last_error());
@@ -519,6 +586,7 @@ int ftar_drain_bg(ftar_comm *c)
 
 int ftar_run_bg(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
+    note_segs(c, dtype, segs, nseg);
     int rc = fdev_run_bg(c->dev, dtype, op, segs, nseg, tag);
     if (rc) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
@@ -529,6 +597,7 @@ int ftar_run_bg(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg,
 
 int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
+    note_segs(c, dtype, segs, nseg);
     int rc = fdev_run(c->dev, dtype, op, segs, nseg, tag);
     if (rc) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
@@ -621,6 +690,7 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
             }
         }
         c->peer_bytes[w] = s->ws_bytes;
+        c->peer_gen[w] = atomic_load(&s->ws_gen);
     }
     for (int w = 0; w < c->wsize; w++) /* the old mappings, dead ranks' included */
         for (int b = 0; b < FTAR_NBUF; b++)

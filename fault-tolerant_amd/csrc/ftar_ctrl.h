@@ -25,9 +25,12 @@
 #include "ftar_dev.h"
 
 #define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
-#define FTAR_SHM_VERSION 3
+#define FTAR_SHM_VERSION 4
 #define FTAR_NBUF 4       /* exported workspace buffers per rank (IN, W, T, R) */
 #define FTAR_DECISIONS 64 /* ring of agree decisions */
+
+#define FTAR_INFLIGHT_LOCAL 1
+#define FTAR_INFLIGHT_PULL 2
 
 #define FTAR_SLOT_EMPTY 0
 #define FTAR_SLOT_RUNNING 2
@@ -65,6 +68,11 @@ typedef struct {
     _Atomic uint64_t done;
     /* BARRIER kill point (tests): reached round `dying`'s barrier and will die there */
     _Atomic uint64_t dying;
+    /* what this rank's stream runs right now: 0 nothing, FTAR_INFLIGHT_LOCAL a kernel on
+     * its own memory, FTAR_INFLIGHT_PULL a kernel reading peers' HBM (an exchange).  Set at
+     * launch, cleared when the stream drained; read post mortem by the launcher (ftrun)
+     * to say whether a killed rank died mid-exchange. */
+    _Atomic int inflight;
     char pad[64];
 } ftar_slot;
 

@@ -81,6 +81,21 @@ bool host_same_va(const hipPointerAttribute_t &a)
     return a.type == hipMemoryTypeHost && a.hostPointer && a.hostPointer == a.devicePointer;
 }
 
+// [ptr, ptr + bytes) inside ONE allocation the runtime knows (device memory, or pinned host
+// memory: hipHostMalloc / hipHostRegister ranges are tracked like device allocations).  A
+// range running past its allocation would be launched on and fault the GPU.
+bool range_inside(const void *ptr, size_t bytes)
+{
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess || !base) {
+        (void)hipGetLastError();
+        return false;
+    }
+    size_t off = (size_t)((const char *)ptr - (const char *)base);
+    return off <= size && bytes <= size - off;
+}
+
 } // namespace
 
 struct ftar_dev {
@@ -297,16 +312,10 @@ int fdev_check_ptr(ftar_dev *d, const void *ptr, size_t bytes)
         return 1; // not memory the runtime knows (pageable host memory)
     }
     if (a.type == hipMemoryTypeUnregistered) return 1;
-    if (a.type == hipMemoryTypeHost) return !host_same_va(a);
+    if (a.type == hipMemoryTypeHost) return !host_same_va(a) || !range_inside(ptr, bytes);
     if (a.type == hipMemoryTypeDevice) {
         if (a.device != d->device) return 1; // another GPU's memory: the kernels run on ours
-        hipDeviceptr_t base = nullptr;     // the whole range inside one allocation
-        size_t size = 0;
-        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
-            (void)hipGetLastError();
-            return 1;
-        }
-        if ((size_t)((const char *)ptr - (const char *)base) + bytes > size) return 1;
+        if (!range_inside(ptr, bytes)) return 1; // the whole range inside one allocation
     }
     return 0;
 }
@@ -727,15 +736,9 @@ static int check_local_ptr(const void *ptr, size_t bytes, int dev)
         (void)hipGetLastError();
         return 1;
     }
-    if (a.type == hipMemoryTypeHost) return !host_same_va(a);
+    if (a.type == hipMemoryTypeHost) return !host_same_va(a) || !range_inside(ptr, bytes);
     if (a.type != hipMemoryTypeDevice || a.device != dev) return 1;
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
-        (void)hipGetLastError();
-        return 1;
-    }
-    return (size_t)((const char *)ptr - (const char *)base) + bytes > size;
+    return !range_inside(ptr, bytes);
 }
 
 int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream)

@@ -45,6 +45,7 @@ struct ftar_comm {
     size_t ws_bytes;
     void *peer[FTAR_MAX_RANKS][FTAR_NBUF];
     size_t peer_bytes[FTAR_MAX_RANKS];
+    uint64_t peer_gen[FTAR_MAX_RANKS]; /* the peer's ws_gen our mappings of its workspace belong to */
 
     const void *uin; /* the current call's buffers (WS_UIN / WS_UOUT) */
     void *uout;
@@ -84,7 +85,13 @@ struct ftar_comm {
     int mesh;            /* FTAR_MESH (default 1): one-hop Raben at power-of-two p without a spare */
     size_t oneshot_max;  /* FTAR_ONESHOT_MAX bytes: mesh Raben in one launch up to this size */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
+    /* the step's last peer read (FTAR_LOOP_SECONDS re-pulls it into pad while it waits) */
+    const void *pad_src;
+    size_t pad_bytes;
+    void *pad; /* local scratch of FTAR_PAD_BYTES, allocated on the first padded step */
 };
+
+#define FTAR_PAD_BYTES ((size_t)16 << 20)
 
 size_t ftar_esize(int dtype);
 int ftar_check_op(int dtype, int op);
@@ -107,6 +114,10 @@ int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
 void ftar_resolve_inputs(ftar_comm *c);
 /* End of a call: IN is the workspace buffer again everywhere. */
 void ftar_inputs_done(ftar_comm *c);
+/* This call's input of original rank w as peers may read it after w died: w's exported
+ * sbuf mapping or its staged IN, only if w published it for THIS call and our mapping
+ * belongs to w's current workspace generation and covers `bytes`; NULL otherwise. */
+const void *ftar_dead_input(ftar_comm *c, int w, size_t bytes);
 
 /* agree over the survivors; returns newly failed original ranks (not yet acked) */
 uint64_t ftar_sync(ftar_comm *c);
@@ -121,6 +132,9 @@ void ftar_sync_fatal(ftar_comm *c);
 int ftar_drain(ftar_comm *c);
 /* enqueue one segment kernel */
 int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+/* bookkeeping of every launch: the control slot's in-flight word (FTAR_INFLIGHT_*) and,
+ * for a peer read (`remote` != NULL, `bytes` of it), the step's re-pull source */
+void ftar_note_launch(ftar_comm *c, const void *remote, size_t bytes);
 /* enqueue on the background stream (after the main stream's current work) */
 int ftar_run_bg(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
 int ftar_drain_bg(ftar_comm *c);

@@ -175,7 +175,19 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
              * peers' mappings hold its memory), so the copy need not cross a link in every
              * call to make a recovery possible. */
             void *W = c->ws[WS_W], *IN = ftar_local(c, WS_IN);
-            const void *D0 = x->keep_recov ? (const void *)c->ws[WS_T] : ftar_buf(c, x->in0_w[vdead], WS_IN);
+            /* Failure model of the elided copy (deviation 6): the dead process's
+             * memory outlives it through the peers' mappings (process death), but not a lost
+             * or reset device.  The read happens only if the dead rank published that input
+             * for this call and our mapping belongs to its current workspace generation;
+             * otherwise there is no redundancy to replay from and the job aborts, the
+             * reference's rule for an unrecoverable failure (errhandler.c:207-211). */
+            const void *D0 = x->keep_recov ? (const void *)c->ws[WS_T]
+                                           : ftar_dead_input(c, x->in0_w[vdead], x->count * x->es);
+            if (!D0) {
+                fprintf(stderr, "ftar: rank %d: the dead rank's step-0 input is not readable: no redundancy\n",
+                        c->wrank);
+                ftar_abort(c, 1);
+            }
             run_reduce(x, at(x, W, dri[0]), at(x, IN, dri[0]), at(x, (void *)D0, dri[0]), drc[0],
                        x->keep_recov ? 0 : FDEV_REMOTE_Y, FDEV_TAG_RECOV);
             for (int s = 1; s <= fs; s++) {
@@ -302,6 +314,7 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
         if (j) remote |= 1u << j;
     }
     double lb0 = ftar_link_bytes(c);
+    ftar_note_launch(c, src[1], (size_t)own_n * x->es);
     if (fdev_tree(c->dev, x->dtype, x->op, src, p, remote, at(x, W, own0), (size_t)own_n, FDEV_TAG_STEP0)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
@@ -389,6 +402,11 @@ static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
         }
     }
     double lb0 = ftar_link_bytes(c);
+    for (int k = 0; k < p * p; k++) /* the first peer operand: the padding's re-pull source */
+        if (remote[k / p] & (1u << (k % p))) {
+            ftar_note_launch(c, src[k], n[k / p] * x->es);
+            break;
+        }
     if (fdev_tree_batch(c->dev, x->dtype, x->op, src, p, remote, out, n, p, FDEV_TAG_STEP0)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);

@@ -170,6 +170,7 @@ void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int n
         if (!t.remote) {
             local[nl++] = t;
         } else if (t.kind == FDEV_COPY) {
+            ftar_note_launch(c, t.x, t.n * es);
             rc = fdev_copy(c->dev, bg, t.out, t.x, t.n * es, 1, tag);
             if (t.out2) /* the second destination from the landed copy (same stream) */
                 local[nl++] = (fdev_seg){FDEV_COPY, 0, t.out2, t.out, NULL, t.n, NULL};
@@ -180,6 +181,7 @@ void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int n
                 continue;
             }
             const void *src = (t.remote & FDEV_REMOTE_X) ? t.x : t.y;
+            ftar_note_launch(c, src, t.n * es);
             rc = fdev_copy(c->dev, bg, stage, src, t.n * es, 1, tag);
             if (t.remote & FDEV_REMOTE_X) t.x = stage;
             else t.y = stage;

@@ -171,10 +171,23 @@ int main(int argc, char **argv)
             p = waitpid(-1, &st, WNOHANG);
         }
         if (p > 0) {
+            int who = -1;
             for (int r = 0; r < np; r++)
-                if (g_pids[r] == p) g_pids[r] = -1;
+                if (g_pids[r] == p) {
+                    g_pids[r] = -1;
+                    who = r;
+                }
             alive--;
             if (WIFSIGNALED(st)) signalled++;
+            if (WIFSIGNALED(st) && who >= 0 && !atomic_load(&job.shm->abort_flag)) {
+                /* post mortem of a killed rank (kill_procs.sh's SIGKILL, an injected kill):
+                 * its control slot says what its stream was running when it died */
+                int inf = atomic_load(&job.shm->slot[who].inflight);
+                fprintf(stderr, "ftrun: rank %d (pid %d) killed by signal %d %s\n", who, (int)p, WTERMSIG(st),
+                        inf == FTAR_INFLIGHT_PULL    ? "mid-exchange: a kernel reading peers' HBM in flight"
+                        : inf == FTAR_INFLIGHT_LOCAL ? "with a local kernel in flight"
+                                                     : "between kernels (no kernel in flight)");
+            }
             else if (WIFEXITED(st) && WEXITSTATUS(st) != 0 && !exit_code) exit_code = WEXITSTATUS(st);
             continue;
         }

@@ -22,7 +22,7 @@ devmap = a[a.index("--devmap") + 1]
 calls = int(a[-1])
 kill = os.environ.get("FTAR_KILL")
 with open(os.environ["FAKE_LOG"], "a") as f:
-    f.write(json.dumps({"argv": a, "kill": kill}) + "\n")
+    f.write(json.dumps({"argv": a, "kill": kill, "redundancy": os.environ.get("FTAR_REDUNDANCY")}) + "\n")
 victim, kc = (int(kill.split(":")[0]), int(kill.split(":")[4])) if kill else (-1, -1)
 full = float(sum(range(n)))
 for r in range(n):
@@ -57,9 +57,14 @@ def bench(tmp_path, monkeypatch):
     return m, tmp_path
 
 
+def _deadline(s=60.0):
+    import time
+    return time.monotonic() + s
+
+
 def test_c5_leg_summary(bench):
     m, tmp = bench
-    res = m.c5_leg(8, list(range(8)), 1024, 9)
+    res = m.c5_leg(8, list(range(8)), 1024, 9, _deadline())
     assert res["devmap"] == [0, 0, 1, 2, 3, 4, 5, 6, 7]  # ranks 0, 1 (pre-step pair + idle spare) on GPU 0
     assert res["recovered"] is True, res
     assert res["kill"].startswith("6:1:1:3 in call 2")
@@ -74,14 +79,19 @@ def test_c5_leg_summary(bench):
     assert res["recovered_rs"] and res["recovered_ag"] and res["recovered_ag_call_ms"] == 3.5
     assert res["kill_ag"].startswith("6:2:1:3 in call 2")
     runs = [json.loads(l) for l in open(tmp / "log.jsonl")]
-    assert [r["kill"] for r in runs] == [None, "6:1:1:3:2", "6:2:1:3:2"]
+    # both recovery shapes: the default, then the reference's (FTAR_REDUNDANCY=1)
+    assert [r["kill"] for r in runs] == [None, "6:1:1:3:2", "6:2:1:3:2"] * 2
+    assert [r["redundancy"] for r in runs] == [None] * 3 + ["1"] * 3
     assert runs[0]["argv"][-3:] == ["raben", "1024", "6"]
+    ref = res["reference_shape"]
+    assert ref["recovered"] and ref["recovered_rs"] and ref["recovered_ag"], ref
+    assert ref["no_fault"]["survivors"] == 9 and ref["fault"]["survivors"] == 8
 
 
 def test_c5_leg_rehearsal_layout(bench):
     """One GPU, 5 ranks (FTAR_C5_RANKS): the victim is the last rank."""
     m, _ = bench
-    res = m.c5_leg(2, [0], 64, 5)
+    res = m.c5_leg(2, [0], 64, 5, _deadline())
     assert res["devmap"] == [0, 0, 0, 0, 0] and res["kill"].startswith("4:1:1:3 in call 2")
     assert res["kill_ag"].startswith("4:2:0:3 in call 2")  # two AG steps: the last one recovers
     assert res["recovered"] is True, res
@@ -92,7 +102,7 @@ def test_c5_leg_wrong_sum_is_not_recovered(bench, monkeypatch):
     m, tmp = bench
     f = tmp / "fault-tolerant_amd" / "bin" / "ftrun"
     f.write_text(FAKE_FTRUN.replace('"value": full - victim if after else full', '"value": full'))
-    res = m.c5_leg(8, list(range(8)), 1024, 9)
+    res = m.c5_leg(8, list(range(8)), 1024, 9, _deadline())
     assert res["recovered"] is False
     assert not all(c["result_ok"] for c in res["fault"]["calls"])
 
@@ -108,27 +118,160 @@ def test_side_legs_run_on_rank0_before_torch(bench, monkeypatch):
     monkeypatch.setenv("MASTER_PORT", f"t{os.getpid()}")
     calls = []
 
-    def c5(world, devices, count, ranks):
+    def c5(world, devices, count, ranks, deadline):
         calls.append((world, devices, count, ranks))
         raise RuntimeError("leg failed")
 
     monkeypatch.setattr(m, "c5_leg", c5)
-    monkeypatch.setattr(m, "cpu_schedule", lambda *a: (_ for _ in ()).throw(OSError("no cores")))
+    monkeypatch.setattr(m, "c5_campaign", lambda *a, **k: {"stub": True})
+    monkeypatch.setattr(m, "cpu_schedule", lambda *a, **k: (_ for _ in ()).throw(OSError("no cores")))
     monkeypatch.setenv("FTAR_C5_RANKS", "9")
-    args = argparse.Namespace(count=1 << 10, no_cpu_baseline=False, no_c5=False, no_xgmi=True)
+    args = argparse.Namespace(count=1 << 10, no_cpu_baseline=False, no_c5=False, no_xgmi=True, side_budget=30.0,
+                              c5_draws=2)
     had_torch = "torch" in sys.modules
     flag = m.leg_flag("side")
     assert not os.path.exists(flag)
     try:
-        cpu, c5r, xg = m.side_legs(args, 0, 8, list(range(8)), False)
+        cpu, c5r, xg, info = m.side_legs(args, 0, 8, list(range(8)), False)
         assert os.path.exists(flag)
         assert calls == [(8, list(range(8)), 1 << 10, 9)]
-        assert c5r == {"error": "leg failed"} and xg is None
+        assert c5r == {"error": "leg failed", "random_kill_campaign": {"stub": True}} and xg is None
         assert cpu["value"] is None and "no cores" in cpu["sample"] and cpu["cores"] == 8
-        assert m.side_legs(args, 3, 8, list(range(8)), False) == (None, None, None)
+        assert info["c5"]["status"] == "error" and info["cpu_baseline"]["status"] == "error"
+        assert m.side_legs(args, 3, 8, list(range(8)), False) == (None, None, None, None)
         assert len(calls) == 1
         if not had_torch:
             assert "torch" not in sys.modules
     finally:
         if os.path.exists(flag):
             os.unlink(flag)
+
+
+def test_run_proc_kills_the_whole_group(bench):
+    """A side-leg job past its deadline is killed with every process it forked (ftrun's
+    ranks are in the launcher's process group)."""
+    import time
+    m, tmp = bench
+    pidfile = tmp / "child.pid"
+    t0 = time.monotonic()
+    rc, out, err, to = m.run_proc(["bash", "-c", f"sleep 300 & echo $! > {pidfile}; wait"], 1.5)
+    assert to and time.monotonic() - t0 < 10
+    child = int(pidfile.read_text())
+    time.sleep(0.2)
+    assert not os.path.exists(f"/proc/{child}") or open(f"/proc/{child}/stat").read().split()[2] == "Z"
+
+
+def test_side_leg_past_its_deadline_is_recorded(bench, monkeypatch):
+    """FTAR_BENCH_HANG=c5: the configs[4] leg's stand-in job never ends; the side legs still
+    end inside their one budget, the leg reads "timeout" and the campaign gets the rest."""
+    import argparse
+    import time
+    m, tmp = bench
+    monkeypatch.setenv("MASTER_PORT", f"h{os.getpid()}")
+    monkeypatch.setenv("FTAR_BENCH_HANG", "c5")
+    monkeypatch.setattr(m, "cpu_schedule", lambda *a, **k: ({"time_s": 0.1, "algbw_GBps": 1.0,
+                                                              "cpu_s_per_rank_whole_process": 0.1}, "cpu"))
+    seen = []
+    monkeypatch.setattr(m, "c5_campaign", lambda dev, count, ranks, d, draws=10: seen.append(d - time.monotonic())
+                        or {"draws_run": 0})
+    args = argparse.Namespace(count=1 << 10, no_cpu_baseline=False, no_c5=False, no_xgmi=True, side_budget=8.0,
+                              c5_draws=2)
+    t0 = time.monotonic()
+    try:
+        cpu, c5r, xg, info = m.side_legs(args, 0, 8, list(range(8)), False)
+    finally:
+        flag = m.leg_flag("side")
+        if os.path.exists(flag):
+            os.unlink(flag)
+    took = time.monotonic() - t0
+    assert took < 8.0 + 3.0, took
+    assert info["c5"]["status"] == "timeout" and "killed" in c5r["error"], (info, c5r)
+    assert cpu["value"] and info["cpu_baseline"]["status"] == "ok"
+    assert seen and 0 < seen[0] <= 8.0 * 0.65 + 0.5  # the campaign runs on what is left
+
+
+def test_north_star_block_prices():
+    """FT Raben moves 2.25 S per rank and direction at p = 8 over one link per
+    step; at B_link = 153.6 GB/s t_roof = 3.93 ms and the 70 % target is algbw >= 47.8 GB/s."""
+    spec = importlib.util.spec_from_file_location("bench_ns", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    S = 256 << 20
+    ns = m.north_star_block(8, S, 5.0e-3, "mesh", None, 7, 2.0 * S / 8)
+    row = ns["priced"]["survey_153.6_assumed"]
+    assert abs(row["t_roof_ms"] - 3.9322) < 1e-3 and abs(row["target_algbw_GBps"] - 47.78) < 0.05
+    assert ns["basis"] == "survey_153.6_assumed" and ns["frac"] == round(3.9322e-3 / 5.0e-3, 4)
+    assert ns["met"] is True and ns["applies"]
+    assert abs(ns["priced"]["nominal_76.8_assumed"]["t_roof_ms"] - 7.8643) < 1e-3
+    cal = m.north_star_block(8, S, 5.0e-3, "mesh", 60.0, 7, 2.0 * S / 8, t_ref=12e-3)
+    assert cal["basis"] == "calibrated"
+    t_roof = 2.25 * S / 60e9
+    assert cal["frac"] == round(t_roof / 5e-3, 4) and cal["met"] == (t_roof / 5e-3 >= 0.7)
+    assert cal["priced"]["calibrated"]["reference_shape"]["frac"] == round(t_roof / 12e-3, 4)
+    assert cal["priced"]["calibrated"]["schedule_t_roof_ms"] == round(2.0 * S / 8 / 60e9 * 1e3, 4)
+    reh = m.north_star_block(2, S, 1e-3, "mesh-oneshot", None, 1, S, rehearsal=True)
+    assert reh["frac"] is None and reh["met"] is None and reh["rehearsal"]
+
+
+def _torchrun_cpu(tmp_path, extra_env, extra_args, timeout):
+    import socket
+    import subprocess
+    import sys
+    import time
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, FTAR_BENCH_CPU_TEST="1", FTAR_HOSTSIM_TAG=f"bench{os.getpid()}", **extra_env)
+    for k in ("FTAR_JOB", "FTAR_RANK", "FTAR_SIZE", "FTAR_LAUNCHER", "FTAR_KILL", "FTAR_DEVICE"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--dist-backend", "gloo", "--count", "65536", "--steps", "3", "--warmup", "1"] + extra_args
+    t0 = time.monotonic()
+    cp = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
+    subprocess.run(f"rm -f /dev/shm/ftarhs-bench{os.getpid()}-*", shell=True)
+    lines = [json.loads(l) for l in cp.stdout.splitlines() if l.startswith("{")]
+    return cp, lines, time.monotonic() - t0
+
+
+@pytest.mark.timeout(240)
+def test_bench_multi_headline_survives_hung_and_failing_legs(hostsim, tmp_path):
+    """The N > 1 line under the driver's launch line (torchrun, 2 ranks), on CPU with the
+    host-sim library: the configs[4] side leg hangs past its deadline, one transport and the
+    RD leg fail.  The headline line is printed right after configs[3] is timed, with the
+    contract's keys and the north-star block; the final line completes with every leg's
+    fate recorded, inside the budgets."""
+    cp, lines, took = _torchrun_cpu(tmp_path, {"FTAR_BENCH_HANG": "c5", "FTAR_BENCH_FAIL": "transports:direct,rd"},
+                                    ["--side-budget", "20", "--c5-draws", "1"], 200)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    assert [d["line"] for d in lines] == ["headline", "final"], cp.stdout[-2000:]
+    head, fin = lines
+    for d in lines:
+        for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                  "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "north_star"):
+            assert k in d, k
+        assert d["value"] > 0 and d["n_gpus"] == 2 and "CPU TEST" in d["data"]
+        ns = d["north_star"]
+        assert ns["target"] and ns["priced"]["survey_153.6_assumed"]["t_roof_ms"] > 0 and "met" in ns
+    assert head["value"] == fin["value"]
+    assert fin["side_legs"]["c5"]["status"] == "timeout" and "killed" in fin["c5_single_kill"]["error"]
+    assert fin["side_legs"]["total_s"] <= 20 + 2
+    assert fin["transports"]["direct"]["error"].startswith("transports:direct: forced failure")
+    assert fin["transports"]["relay2hop"]["raben_ms"] > 0
+    assert fin["legs"]["rd"]["status"] == "error" and fin["rd"] is None
+    assert fin["exact_on_node"]["all_exact"], fin["exact_on_node"]
+    assert fin["int32_rank_checksum_ok"] == {"raben": True, "rd": True}
+    assert fin["cpu_baseline"]["value"] and fin["cpu_baseline"]["cores"] == 2
+    assert took < 150, took
+
+
+@pytest.mark.timeout(240)
+def test_bench_multi_watchdog_prints_and_exits(hostsim, tmp_path):
+    """An optional leg that never returns (FTAR_BENCH_HANG=checks): at the job budget the
+    watchdog prints the line as it stands (marked truncated) and every rank exits cleanly."""
+    cp, lines, took = _torchrun_cpu(tmp_path, {"FTAR_BENCH_HANG": "checks"},
+                                    ["--side-budget", "5", "--budget", "30", "--no-c5", "--no-xgmi"], 200)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    assert [d["line"] for d in lines] == ["headline", "final"], cp.stdout[-2000:]
+    assert "watchdog" in lines[-1]["truncated"] and lines[-1]["value"] == lines[0]["value"]
+    assert took < 30 + 30, took

@@ -4,6 +4,7 @@ Bar: bit-exact for every dtype/op on the same inputs (one IEEE op per element fo
 floats; two's-complement wrap for ints).  Sizes cover empty, ragged, unaligned heads
 and tails, non-co-aligned pointers (scalar path) and the full 256 MiB C2 vector.
 """
+import os
 import numpy as np
 import pytest
 
@@ -260,3 +261,28 @@ def test_reduce_local_refuses_pageable_and_overruns(ftar):
     torch.cuda.synchronize()
     assert bool((y == 2.0).all())
     assert np.array_equal(page, np.arange(4096, dtype=np.float32))
+
+
+def test_short_pinned_buffers_refused(ftar):
+    """A pinned host buffer shorter than `count`: refused with FTAR_ERR_ARG by the
+    local reduce and by both Allreduce entry points before anything is launched -- the GPU
+    would otherwise page-fault past the pinned allocation."""
+    import torch
+    short = torch.ones(1024).pin_memory()
+    y = torch.full((1 << 20,), 2.0).pin_memory()
+    yd = torch.full((1 << 20,), 2.0, device="cuda")
+    for a, b in ((short, yd), (yd, short), (short, y)):
+        with pytest.raises(ftar.FtarError, match="code 13"):
+            ftar.reduce_local(a, b, count=1 << 20, dtype=1)
+    comm = ftar.Comm.init_rank(f"/ftar-pin-{os.getpid()}", 0, 1, 0)
+    try:
+        assert comm.allreduce_rabenseifner(short, yd, count=1 << 20) == ftar.ERR_ARG
+        assert comm.allreduce_rabenseifner(yd, short, count=1 << 20) == ftar.ERR_ARG
+        assert comm.recursive_doubling(short, yd, count=1 << 20) == ftar.ERR_ARG
+        assert comm.recursive_doubling(yd, short, count=1 << 20) == ftar.ERR_ARG
+        # the same buffers at their own length go through (zero copy on pinned memory)
+        assert comm.allreduce_rabenseifner(short, short, count=1024) == 0
+    finally:
+        comm.finalize()
+    torch.cuda.synchronize()
+    assert bool((yd == 2.0).all()) and bool((y == 2.0).all()) and bool((short == 1.0).all())

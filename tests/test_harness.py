@@ -54,6 +54,12 @@ def test_single_kill_is_classified(hostsim, tmp_path, algo):
     assert r["RIGHT RESULT"] == "True"
     assert (r["KILLED"] == "1" and r["ABORT"] == "False") or (r["ABORT"] == "True" and int(r["KILLED"]) == n) \
         or r["KILLED"] == "0", r
+    # the row-side log: the launcher's post mortem names the victim and whether it died
+    # with a pull in flight (the padded steps re-pull their windows, so it mostly does)
+    side = list(csv.DictReader(open(str(tmp_path / f"{algo}_1.csv") + ".victims"), delimiter=";"))
+    assert len(side) == 1 and side[0]["N"] == r["N"] and side[0]["KILLED"] == r["KILLED"], side
+    if r["KILLED"] == "1":
+        assert len(side[0]["VICTIMS"].split()) == 1 and side[0]["MID EXCHANGE"] in ("True", "False"), side
 
 
 @pytest.mark.parametrize("algo", ["raben", "rd"])
@@ -113,3 +119,34 @@ def test_launcher_never_a_kill_candidate(hostsim):
     assert not bad, (bad, launchers)
     assert seen_ranks, "no rank process was ever a candidate"
     assert out.count("Hello from") == 4
+
+
+def test_random_kills_land_mid_exchange(hostsim, tmp_path):
+    """The stretched steps (FTAR_LOOP_SECONDS) re-pull their last peer window instead of
+    idling, so the reference killer's SIGKILL (a random R-state rank after DELAY) meets a
+    pull in flight: at least half of the kills are reported mid-exchange by the launcher."""
+    import re
+    import time
+    exe = os.path.join(ROOT, "tests", "hostsim", "_build", "src", "raben", "main")
+    ftrun = os.path.join(ROOT, "tests", "hostsim", "_build", "bin", "ftrun")
+    mid = total = 0
+    for k in range(6):
+        env = dict(os.environ, FTAR_PROG=exe, FTAR_LOOP_SECONDS="2", FTAR_HOSTSIM_TAG=f"mx{os.getpid()}")
+        proc = subprocess.Popen([ftrun, "-np", "5", "2000000"], env=env, stdout=subprocess.PIPE,
+                                stderr=subprocess.PIPE, text=True)
+        try:
+            time.sleep(0.8 + 0.15 * k)
+            kids = subprocess.run(["ps", "-o", "pid=", "--ppid", str(proc.pid)], capture_output=True,
+                                  text=True).stdout.split()
+            if kids:
+                os.kill(int(kids[k % len(kids)]), 9)
+            out, err = proc.communicate(timeout=60)
+        finally:
+            if proc.poll() is None:
+                proc.kill()
+            subprocess.run(f"rm -f /dev/shm/ftarhs-mx{os.getpid()}-*", shell=True)
+        post = re.findall(r"ftrun: rank \d+ \(pid \d+\) killed by signal 9 (.*)", err)
+        total += len(post)
+        mid += sum(1 for p in post if p.startswith("mid-exchange"))
+    assert total >= 4, total
+    assert mid * 2 >= total, (mid, total)

@@ -691,3 +691,35 @@ def test_kill_logical_bitwise(hostsim, oracle, algo, p, kill, op):
     """A recovering kill under a bitwise op: the handlers' replays and re-sends reduce
     with the call's op (not SUM)."""
     _cmp(_fn(oracle, algo), algo, _bit_inputs(p, 777, p + op, np.int32), [kill], op=op)
+
+
+@pytest.mark.parametrize("p", [5, 9])
+def test_withdrawn_dead_input_aborts(hostsim, oracle, p):
+    """Without the step-0 redundancy copy (the default with a spare), the RS replay reads the
+    dead rank's step-0 input where it lies (deviation 6): a process death leaves
+    it mapped, a lost device does not.  FTAR_KILL_WITHDRAW makes the victim withdraw its input
+    as it dies (its workspace generation moves on, its published sbuf is retracted): the
+    replay must then refuse to read it and the job abort -- never a result from a stale or
+    unmapped buffer.  With the reference's copy (FTAR_REDUNDANCY=1) the same kills recover
+    bit-exact like the oracle, and reduce-scatter kills of the idle spare, which need no
+    replay, recover either way."""
+    ins = oracle.random_inputs(p, 257, seed=p + 7)
+    n_abort = n_rec = 0
+    for v in range(p):
+        for st in (1, 2):
+            for pt in range(4):
+                ks = [(v, 1, st, pt)]
+                o = oracle.rabenseifner(ins, ks)
+                if o.aborted or o.status[v] != oracle.DEAD:
+                    continue
+                replay = v != 1  # rank 1 is the idle odd rank of the pre-step pair (rem = 1)
+                r = H.run_probe("raben", ins, ks, backend="hostsim", env_extra={"FTAR_KILL_WITHDRAW": "1"})
+                if replay:
+                    assert r.aborted and not r.outputs, (ks, r.stderr[-800:])
+                    assert "not readable" in r.stderr, r.stderr[-800:]
+                    n_abort += 1
+                else:
+                    _cmp(oracle.rabenseifner, "raben", ins, ks, env={"FTAR_KILL_WITHDRAW": "1"})
+                    n_rec += 1
+                _cmp(oracle.rabenseifner, "raben", ins, ks, env={"FTAR_KILL_WITHDRAW": "1", "FTAR_REDUNDANCY": "1"})
+    assert n_abort > 0 and n_rec > 0, (n_abort, n_rec)

@@ -18,6 +18,7 @@ import json
 import os
 import re
 import resource
+import signal
 import statistics
 import subprocess
 import sys
@@ -46,7 +47,23 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def run(algo: str, p: int, count: int, dtype: str, reps: int) -> dict:
+def run_proc(cmd, env, timeout):
+    """The job in a process group of its own, SIGKILLed as a whole past `timeout`."""
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+        return p.returncode, out, err, False
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        return p.returncode, out, err, True
+
+
+def run(algo: str, p: int, count: int, dtype: str, reps: int, timeout: float = 1800.0) -> dict:
+    """`reps` calls of the schedule, all of them within `timeout` seconds (a job still
+    running then is killed with its ranks and the run fails)."""
+    deadline = time.monotonic() + timeout
     exe = os.path.join(HS, OUT, "src", algo, "main")
     ftrun = os.path.join(HS, OUT, "bin", "ftrun")
     # the reference's shape: pairwise exchanges step by step (no relay, no mesh)
@@ -55,13 +72,15 @@ def run(algo: str, p: int, count: int, dtype: str, reps: int) -> dict:
     times, cpu = [], []
     for _ in range(reps):
         ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
-        cp = subprocess.run([ftrun, "-np", str(p), exe, str(count)], env=env, capture_output=True, text=True,
-                            timeout=600)
+        rc, out, err, timed_out = run_proc([ftrun, "-np", str(p), exe, str(count)], env,
+                                           max(1.0, deadline - time.monotonic()))
         subprocess.run(f"rm -f /dev/shm/ftarhs-cpub{os.getpid()}-*", shell=True)
-        if cp.returncode != 0:
-            raise RuntimeError(f"{algo} p={p} failed: {cp.stderr[-1000:]}")
-        ts = [float(x) for x in re.findall(r"^Time: (\S+)", cp.stdout, flags=re.M)]
-        hello = re.findall(r"result is: (-?\d+)", cp.stdout)
+        if timed_out:
+            raise TimeoutError(f"{algo} p={p}: still running after {timeout:.0f} s (killed)")
+        if rc != 0:
+            raise RuntimeError(f"{algo} p={p} failed: {err[-1000:]}")
+        ts = [float(x) for x in re.findall(r"^Time: (\S+)", out, flags=re.M)]
+        hello = re.findall(r"result is: (-?\d+)", out)
         expect = ((p * (p - 1) // 2) % 17) * count
         if len(hello) != p or any(int(h) != expect for h in hello):
             raise RuntimeError(f"{algo} p={p}: wrong checksums {hello} (expected {expect})")
