@@ -257,7 +257,12 @@ int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
     me->uid = ok ? id : 0;
     me->uoff = off;
     me->useq = (uint64_t)c->ncalls; /* a rank that dies before this point leaves an older tag */
-    if (ok) c->in_alias = sbuf;
+    if (ok) {
+        c->in_alias = sbuf;
+        /* peers read the caller's memory in place: the drain before the call's first barrier
+         * must write it back device-wide (a fenced marker), whatever this rank launched */
+        fdev_fence_next_drain(c->dev);
+    }
     c->in_bytes = bytes;
     if (c->verbose >= 2) fprintf(stderr, "ftar[%d] call %d: input %s\n", c->wrank, c->ncalls, ok ? "in place" : "staged");
     return ok;
@@ -625,6 +630,34 @@ void ftar_shrink(ftar_comm *c, uint64_t failed)
         if (!(failed & (1ull << c->order[i]))) c->order[k++] = c->order[i];
     c->size = k;
     recompute_members(c);
+}
+
+/* A comm of one rank -- p = 1, or every peer lost -- has no exchange: the result is the
+ * input (raben/util.c:35-42 copy_buffer; rd: N = 1 returns src, DESIGN.md deviation 4).
+ * Nothing is exported or staged and the workspace is not touched: one copy launch (none in
+ * place), one drain and the closing barrier; the kill points of the schedule's pre- and
+ * post-phases are passed in their usual order. */
+int ftar_single_rank(ftar_comm *c, const void *sbuf, void *rbuf, size_t bytes)
+{
+    fdev_order_after(c->dev, c->user_stream);
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BEFORE);
+    ftar_enter(c);
+    if (sbuf != rbuf) {
+        fdev_seg s = {FDEV_COPY, 0, rbuf, sbuf, NULL, bytes / 4, NULL};
+        ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL);
+    }
+    ftar_launched(c, FTAR_PH_PRE, 0);
+    ftar_drain(c);
+    ftar_exchange_done(c);
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BARRIER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
+    ftar_sync_fatal(c);
+    ftar_stats_end(c);
+    return FTAR_SUCCESS;
 }
 
 /* ---- workspace ------------------------------------------------------------ */

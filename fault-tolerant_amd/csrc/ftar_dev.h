@@ -112,6 +112,9 @@ int fdev_order_after(ftar_dev *d, void *user_stream);
 /* Spin (busy, the process stays in R state) until the stream drained.  `poll` is
  * called between queries; a nonzero return aborts the wait with that value. */
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg);
+/* The next fdev_sync must be a fenced marker even if only signalled launches were queued:
+ * peers are about to read memory the caller wrote (its send buffer, read in place). */
+void fdev_fence_next_drain(ftar_dev *d);
 /* 1 while work queued on the rank's stream has not completed (kill-point diagnostics). */
 int fdev_busy(ftar_dev *d);
 

@@ -117,6 +117,19 @@ struct ftar_dev {
     } exp[4];
     unsigned long long exp_clock;
     int export_retries;
+    // Completion signals of short launches (ftar_kernels.h KSignal): a drain
+    // whose stream holds only signalled launches since the previous drain waits for the
+    // kernel's own flag in pinned host memory instead of a fenced marker packet.
+    unsigned *sig_cnt;     // device counter of the signalling workgroups
+    unsigned *sig_flag;    // pinned host word, mapped at the same address
+    unsigned sig_tag;      // tag of the last signalled launch
+    int flag_sync;         // FTAR_FLAG_SYNC (default 1)
+    unsigned flag_max;     // FTAR_FLAG_MAX_BLOCKS: largest grid that signals (default 64)
+    int unsignalled;       // main-stream launches / copies since the last drain without a signal
+    int signalled;         // ... with one
+    int need_acquire;      // the last drain was a signal: no marker has invalidated the caches since
+    int force_fence;       // the next drain must be a fenced marker (peers read caller memory in place)
+    int waited_user;       // a wait on the caller's stream was queued since the last drain
 };
 
 extern "C" {
@@ -155,6 +168,32 @@ int fdev_open(int device, ftar_dev **out)
     // consistent fence -- L2 writeback and invalidation -- see sync_stream
     HIPCHK(hipEventCreateWithFlags(&d->fence_main, hipEventDisableTiming));
     d->fence_bg = nullptr;
+    {
+        const char *fs = getenv("FTAR_FLAG_SYNC"), *fm = getenv("FTAR_FLAG_MAX_BLOCKS");
+        d->flag_sync = fs ? atoi(fs) != 0 : 1;
+        d->flag_max = fm ? (unsigned)atoi(fm) : 64;
+        d->sig_cnt = nullptr;
+        d->sig_flag = nullptr;
+        d->sig_tag = 0;
+        d->unsignalled = d->signalled = d->need_acquire = d->force_fence = d->waited_user = 0;
+        if (d->flag_sync) {
+            HIPCHK(hipMalloc((void **)&d->sig_cnt, 256));
+            HIPCHK(hipMemset(d->sig_cnt, 0, 256));
+            HIPCHK(hipHostMalloc((void **)&d->sig_flag, 256, hipHostMallocCoherent | hipHostMallocMapped));
+            void *dp = nullptr;
+            HIPCHK(hipHostGetDevicePointer(&dp, d->sig_flag, 0));
+            if (dp != (void *)d->sig_flag) { // the kernels store through the host address
+                (void)hipHostFree(d->sig_flag);
+                (void)hipFree(d->sig_cnt);
+                d->sig_flag = nullptr;
+                d->sig_cnt = nullptr;
+                d->flag_sync = 0;
+            } else {
+                __atomic_store_n(d->sig_flag, 0u, __ATOMIC_RELEASE);
+            }
+            HIPCHK(hipDeviceSynchronize());
+        }
+    }
     d->h2d = d->d2h = nullptr;
     d->fence_d2h = nullptr;
     memset(d->h2d_done, 0, sizeof(d->h2d_done));
@@ -191,6 +230,8 @@ void fdev_close(ftar_dev *d)
         if (d->h2d_done[i]) (void)hipEventDestroy(d->h2d_done[i]);
     if (d->fence_d2h) (void)hipEventDestroy(d->fence_d2h);
     if (d->h2d) (void)hipStreamDestroy(d->h2d);
+    if (d->sig_cnt) (void)hipFree(d->sig_cnt);
+    if (d->sig_flag) (void)hipHostFree(d->sig_flag);
     delete d;
 }
 
@@ -366,6 +407,31 @@ static hipEvent_t get_event(ftar_dev *d)
     return e;
 }
 
+// Bookkeeping of every launch or copy on a stream of this rank.  On the main stream: a
+// launch of at most flag_max workgroups that may signal gets the completion signal
+// (returned in *sig).  After a signal drain no marker packet has invalidated the caches
+// (need_acquire): a signalled launch then invalidates them itself, per workgroup, for its
+// own loads (`acquire`; an XCD's invalidate does nothing for the others, so need_acquire
+// stays set), and any other launch is preceded by a fenced marker, which invalidates them
+// device-wide as the drain's marker used to and clears need_acquire.  A background-stream
+// launch gets such a marker on its own stream.
+static void note_launch(ftar_dev *d, hipStream_t st, unsigned grid, bool can_signal, ftar::KSignal *sig)
+{
+    if (sig) *sig = ftar::KSignal{nullptr, nullptr, 0, 0};
+    if (st != d->stream) {
+        if (d->need_acquire && d->fence_bg) (void)hipEventRecord(d->fence_bg, st);
+        return;
+    }
+    if (can_signal && sig && d->flag_sync && grid <= d->flag_max) {
+        *sig = ftar::KSignal{d->sig_cnt, d->sig_flag, ++d->sig_tag, (unsigned)d->need_acquire};
+        d->signalled++;
+    } else {
+        if (d->need_acquire) (void)hipEventRecord(d->fence_main, st);
+        d->need_acquire = 0;
+        d->unsignalled++;
+    }
+}
+
 static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     size_t es = esize_of(dtype);
@@ -392,6 +458,7 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
     if (grid == 0) return 0;
     L.nt_store = nt_store();
+    note_launch(d, st, grid, true, &L.sig);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
         e0 = get_event(d);
@@ -426,6 +493,7 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
         e1 = get_event(d);
         if (e0) (void)hipEventRecord(e0, d->stream);
     }
+    note_launch(d, d->stream, ~0u, false, nullptr);
     // pieces of at most max_blocks vector workgroups (plan_tree refuses larger bodies)
     const size_t piece = (size_t)d->max_blocks * 256 * (16 / es);
     for (size_t off = 0; off < n; off += piece) {
@@ -485,6 +553,7 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
     }
     d->ctr.link_bytes += link;
     d->ctr.hbm_bytes += hbm;
+    note_launch(d, d->stream, grid, true, &B.sig);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
         e0 = get_event(d);
@@ -538,6 +607,7 @@ int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int
     } else {
         d->ctr.hbm_bytes += 2.0 * (double)bytes;
     }
+    note_launch(d, st, ~0u, false, nullptr);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
         e0 = get_event(d);
@@ -554,6 +624,12 @@ int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int
 
 int fdev_order_after(ftar_dev *d, void *user_stream)
 {
+    // an idle caller stream has nothing our kernels must wait for (its kernels completed,
+    // their stores released to this device); queuing the wait costs ~1.3 us
+    hipError_t q = hipStreamQuery((hipStream_t)user_stream);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) (void)hipGetLastError();
+    d->waited_user = 1;
     hipEvent_t e = get_event(d);
     if (!e) return set_err(hipErrorOutOfMemory, "hipEventCreate");
     HIPCHK(hipEventRecord(e, (hipStream_t)user_stream));
@@ -588,12 +664,47 @@ static int sync_stream(ftar_dev *d, hipStream_t st, int (*poll)(void *), void *a
     return 0;
 }
 
+// Waits for the signal of launch `tag` (its last workgroup's store into the pinned flag
+// word), polling the failure detector; a device error surfaces through hipStreamQuery.
+static int wait_signal(ftar_dev *d, unsigned tag, int (*poll)(void *), void *arg)
+{
+    for (unsigned spins = 1;; spins++) {
+        if ((int)(__atomic_load_n(d->sig_flag, __ATOMIC_ACQUIRE) - tag) >= 0) return 0;
+        if (poll) {
+            int r = poll(arg);
+            if (r) return r;
+        }
+        if ((spins & 255) == 0) {
+            hipError_t e = hipStreamQuery(d->stream);
+            if (e == hipSuccess) { // the stream drained: the flag is there, or fall back
+                if ((int)(__atomic_load_n(d->sig_flag, __ATOMIC_ACQUIRE) - tag) >= 0) return 0;
+                return sync_stream(d, d->stream, poll, arg);
+            }
+            if (e != hipErrorNotReady) return set_err(e, "hipStreamQuery");
+        }
+    }
+}
+
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 {
-    int rc = sync_stream(d, d->stream, poll, arg);
+    int rc;
+    if (!d->unsignalled && !d->signalled && !d->waited_user && !d->force_fence) {
+        rc = 0; // nothing queued since the last drain
+    } else if (!d->unsignalled && d->signalled && !d->force_fence) {
+        // only signalled launches: each workgroup released its stores at system scope before
+        // the last one raised the flag, so the data is visible to the peers and the host
+        rc = wait_signal(d, d->sig_tag, poll, arg);
+        d->need_acquire = 1;
+    } else {
+        rc = sync_stream(d, d->stream, poll, arg);
+        d->need_acquire = 0;
+    }
+    d->unsignalled = d->signalled = d->waited_user = d->force_fence = 0;
     if (rc) return rc;
     return harvest(d);
 }
+
+void fdev_fence_next_drain(ftar_dev *d) { d->force_fence = 1; }
 
 int fdev_busy(ftar_dev *d)
 {
@@ -700,12 +811,14 @@ int fdev_sync_d2h(ftar_dev *d, int (*poll)(void *), void *arg)
 
 int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t bytes)
 {
+    note_launch(d, d->stream, ~0u, false, nullptr);
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d->stream));
     return fdev_sync(d, nullptr, nullptr);
 }
 
 int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t bytes)
 {
+    note_launch(d, d->stream, ~0u, false, nullptr);
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, d->stream));
     return fdev_sync(d, nullptr, nullptr);
 }

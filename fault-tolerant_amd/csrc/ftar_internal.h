@@ -153,6 +153,9 @@ void ftar_exchange_done(ftar_comm *c);
  * its side of the exchange -- mid-transfer included (FTAR_PT_DURING). */
 int ftar_peer_done(ftar_comm *c, int w);
 
+/* the whole call on a comm of one rank (both schedules): copy, drain, closing barrier */
+int ftar_single_rank(ftar_comm *c, const void *sbuf, void *rbuf, size_t bytes);
+
 /* deterministic fault injection at (phase, step, point) */
 void ftar_maybe_die(ftar_comm *c, int phase, int step, int point);
 

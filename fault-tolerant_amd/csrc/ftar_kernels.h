@@ -16,6 +16,22 @@ constexpr int kTileVecs = 1024; // 16-byte vectors per workgroup tile (256 threa
 constexpr int kChunkTiles = 8; // tiles per chunk of the interleaved block mapping (128 KiB)
 constexpr int kMaxIleave = 16; // vector pieces that can share the interleaved prefix
 
+// Completion signal of a short launch (the small-message path): instead of a
+// marker packet the host spins on, the kernel itself tells the host it is done.  Every
+// workgroup, once its stores have completed, releases them at system scope (write-back of
+// its XCD's L2: the data is in HBM for peer GPUs and the host) and adds one to `cnt`; the
+// workgroup whose add completes the grid resets `cnt` and stores `tag` into `flag`, a word of
+// pinned host memory the host polls.  `acquire`: every workgroup first invalidates its
+// cached copies of remote memory (system-scope acquire) -- the host sets it when the last
+// drain was such a signal, i.e. no marker packet has invalidated the caches since the
+// barrier after which this launch reads the peers' new data.
+struct KSignal {
+    unsigned *cnt;  // device counter, agent-scope atomics; nullptr = no signal
+    unsigned *flag; // pinned host word
+    unsigned tag;
+    unsigned acquire;
+};
+
 struct KSeg {
     void *out;
     void *out2;          // optional second destination (same values), nullptr = none
@@ -41,6 +57,7 @@ struct KSegList {
     unsigned il_blocks;
     unsigned char il[kMaxIleave];
     unsigned nt_store; // 16-byte stores non-temporal (set by the caller after plan_segments)
+    KSignal sig;       // optional completion signal (sig.cnt == nullptr: none)
 };
 
 // What one workgroup of segment_kernel processes: piece `seg`, starting at tile (vector
@@ -105,6 +122,7 @@ struct TreeBatch {
     TreeArgs t[kMaxBatch];
     unsigned first[kMaxBatch + 1];
     int nt;
+    KSignal sig; // optional completion signal
 };
 unsigned plan_tree_batch(TreeBatch *B, int p, size_t esize, unsigned max_blocks);
 hipError_t launch_tree_batch(int dtype, int op, int p, const TreeBatch &B, unsigned grid, hipStream_t s);

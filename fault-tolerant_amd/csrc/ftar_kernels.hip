@@ -132,6 +132,32 @@ __device__ __forceinline__ void st16(uint4 *p, uint4 v, unsigned nts)
     }
 }
 
+// KSignal (ftar_kernels.h): optional acquire before the first load, release + completion
+// flag after the last store.  The branch is uniform over the launch.
+__device__ __forceinline__ void signal_acquire(const KSignal &G)
+{
+    if (G.cnt && G.acquire) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system scope: drop cached remote lines
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+__device__ __forceinline__ void signal_done(const KSignal &G)
+{
+    if (!G.cnt) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's stores have completed
+    __syncthreads();                                  // ... and every other wave's
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // system scope: this XCD's dirty lines to HBM
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the write-back completed (never elided)
+        const unsigned old = __hip_atomic_fetch_add(G.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gridDim.x - 1) { // every workgroup has released: the launch is done
+            __hip_atomic_store(G.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(G.flag, G.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 template <typename T, int OP>
 __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk, unsigned nts)
 {
@@ -196,8 +222,10 @@ __global__ __launch_bounds__(kBlock) void segment_kernel(KSegList L)
     const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     const BlockWork w = map_block(L, b);
     const KSeg &S = L.s[__builtin_amdgcn_readfirstlane(w.seg)];
+    signal_acquire(L.sig);
     if (S.vec) vec_body<T, OP>(S, w.first, w.stride, L.nt_store);
     else scalar_body<T, OP>(S, w.first, w.stride);
+    signal_done(L.sig);
 }
 
 // LDS-DMA staged local reduce (variant 1): the `in` operand is moved HBM -> LDS by
@@ -287,7 +315,9 @@ __global__ __launch_bounds__(kBlock) void tree_batch_kernel(TreeBatch B)
     const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     int k = 0;
     while (k + 1 < B.nt && b >= B.first[k + 1]) k++;
+    signal_acquire(B.sig);
     tree_body<T, OP, P>(B.t[k], b - B.first[k], B.first[k + 1] - B.first[k]);
+    signal_done(B.sig);
 }
 
 // ---------------------------------------------------------------------------------
@@ -436,6 +466,7 @@ unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_bloc
 {
     L->nseg = 0;
     L->nt_store = 0;
+    L->sig = KSignal{nullptr, nullptr, 0, 0};
     size_t vec_bytes_total = 0;
     struct Piece { KSeg k; size_t bytes; } pieces[kMaxKSegs];
     int np = 0;

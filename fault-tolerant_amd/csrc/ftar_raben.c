@@ -354,15 +354,16 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
     c->stats.mesh_steps++;
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_AFTER);
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BARRIER);
-    newf = ftar_step_sync(c, 2); /* (:330-335) */
-    if (newf) rb_handler_ag(x, newf, 0); /* no idle rank: aborts */
-
-    /* ERRORS_ARE_FATAL barrier (:357-360); no post-step at rem = 0 */
+    /* The allgather's agree (:330-335) and the ERRORS_ARE_FATAL barrier (:357-360; no
+     * post-step at rem = 0) are one round: a failure seen at either ends the job the same
+     * way (no idle rank: errhandler_allgather aborts, new_entry = -1, :377-378), so the
+     * outcome of every kill point is unchanged. */
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
-    ftar_sync_fatal(c);
+    newf = ftar_step_sync(c, 2);
+    if (newf) rb_handler_ag(x, newf, 0); /* no idle rank: aborts */
     ftar_stats_end(c);
     return FTAR_SUCCESS;
 }
@@ -420,8 +421,11 @@ static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
     c->stats.mesh_steps++;
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_AFTER);
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BARRIER);
-    uint64_t newf = ftar_step_sync(c, 2); /* agree + barrier (:258-265) */
-    if (newf) rb_handler_rs(x, newf, L - 1); /* no idle rank: aborts */
+    /* The reduce-scatter's agree (:258-265), the allgather's (:330-335) and the
+     * ERRORS_ARE_FATAL barrier (:357-360) are one round here: the allgather's data moved in
+     * the same launch, and with no idle rank a failure seen at any of them ends the job the
+     * same way (both handlers abort, new_entry = -1, errhandler.c:207-211, 377-378) -- the
+     * kill points of every phase are passed before it, so each one's outcome is unchanged. */
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
     ftar_enter(c); /* the allgather's data already moved in the one launch */
     ftar_launched(c, FTAR_PH_AG, L - 1);
@@ -429,13 +433,12 @@ static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
     ftar_exchange_done(c);
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_AFTER);
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BARRIER);
-    newf = ftar_step_sync(c, 2); /* (:330-335) */
-    if (newf) rb_handler_ag(x, newf, 0); /* no idle rank: aborts */
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
     ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
-    ftar_sync_fatal(c);
+    uint64_t newf = ftar_step_sync(c, 1);
+    if (newf) rb_handler_rs(x, newf, L - 1); /* no idle rank: aborts */
     ftar_stats_end(c);
     return FTAR_SUCCESS;
 }
@@ -492,6 +495,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);
+    if (c->size == 1) return ftar_single_rank(c, sbuf, rbuf, count * x->es);
 
     size_t bytes = count * x->es;
     ftar_ensure_workspace(c, bytes);

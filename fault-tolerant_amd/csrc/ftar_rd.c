@@ -183,6 +183,7 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     c->uin = src;
     c->uout = dst;
     ftar_stats_begin(c);
+    if (c->size == 1) return ftar_single_rank(c, src, dst, count * x->es);
     int me = c->wrank;
 
     size_t bytes = count * x->es;

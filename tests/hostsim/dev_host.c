@@ -296,6 +296,7 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 }
 
 int fdev_busy(ftar_dev *d) { return 0; } /* host "kernels" complete at launch */
+void fdev_fence_next_drain(ftar_dev *d) {}
 
 int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t n)
 {

@@ -54,7 +54,7 @@ def main():
             comm.set_option(ftar.OPT_ONESHOT_MAX, limit)
             for _ in range(5):
                 assert fn(x, y) == 0
-            wall, drain, sync, kern = [], [], [], []
+            wall, drain, sync, kern, cwall = [], [], [], [], []
             for _ in range(200):
                 comm.barrier()
                 t0 = time.perf_counter()
@@ -64,8 +64,12 @@ def main():
                 drain.append(st.drain_s)
                 sync.append(st.sync_wait_s)
                 kern.append(st.step0_kernel_ms * 1e-3)
+                cwall.append(st.wall_s)
             key = name + ("_profiled" if prof else "")
-            res[key] = {"wall_us": med(wall), "drain_us": med(drain), "sync_wait_us": med(sync)}
+            # wall: the Python call; c_wall: inside the C entry point (ftar_stats wall_s,
+            # what a C caller of include/ftar.h pays, minus the argument checks)
+            res[key] = {"wall_us": med(wall), "c_wall_us": med(cwall), "drain_us": med(drain),
+                        "sync_wait_us": med(sync)}
             if prof:
                 res[key]["step0_kernel_us"] = med(kern)
     comm.set_option(ftar.OPT_ONESHOT_MAX, 1 << 20)
