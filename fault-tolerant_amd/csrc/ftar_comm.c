@@ -159,6 +159,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
     c->oneshot_max = getenv("FTAR_ONESHOT_MAX") ? (size_t)atoll(getenv("FTAR_ONESHOT_MAX")) : ((size_t)1 << 20);
     c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
+    c->stage_max = getenv("FTAR_STAGE_MAX") ? (size_t)atoll(getenv("FTAR_STAGE_MAX")) : ((size_t)1 << 20);
     c->host_pipe = getenv("FTAR_HOST_PIPE") ? atoi(getenv("FTAR_HOST_PIPE")) : 1;
     c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)4 << 20);
     int create = getenv("FTAR_LAUNCHER") == NULL;
@@ -253,6 +254,9 @@ int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
     uint64_t id = 0;
     size_t off = 0;
     ftar_inputs_done(c);
+    /* a small input is cheaper staged than read in place: the staging copy signals its own
+     * completion, where peers reading the caller's memory need a fenced marker */
+    if (bytes <= c->stage_max) alias_ok = 0;
     int ok = alias_ok && c->export_user && bytes && fdev_export_range(c->dev, sbuf, bytes, me->uhandle, &id, &off) == 0;
     me->uid = ok ? id : 0;
     me->uoff = off;

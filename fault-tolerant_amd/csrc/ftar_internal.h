@@ -65,6 +65,7 @@ struct ftar_comm {
     void *peer_in[FTAR_MAX_RANKS];
     uint64_t last_uid[FTAR_MAX_RANKS]; /* peers' published allocation ids in the last call */
     int export_user;     /* FTAR_EXPORT (default 1): let peers read sbuf in place where possible */
+    size_t stage_max;    /* FTAR_STAGE_MAX bytes: inputs up to this size are staged, never read in place */
     int host_pipe;       /* FTAR_HOST_PIPE (default 1): chunk-pipelined host-buffer Raben where it applies */
 
     /* host staging for the _host entry points */

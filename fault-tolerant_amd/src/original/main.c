@@ -125,9 +125,12 @@ int main(int argc, char *argv[])
     CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
 
     void *buffer = malloc(bytes + 4), *result = malloc(bytes + 4);
+    /* FTAR_FILL_OFFSET=k (default 0, the reference's input): buffer[i] = rank + k, so a one-rank
+     * run has a nonzero checksum, ((N(N-1)/2 + N k) % 17) * count */
+    const int fill = getenv("FTAR_FILL_OFFSET") ? atoi(getenv("FTAR_FILL_OFFSET")) : 0;
     for (int i = 0; i < buf_size; i++) {
-        if (is_float) ((float *)buffer)[i] = (float)rank;
-        else ((int *)buffer)[i] = rank;
+        if (is_float) ((float *)buffer)[i] = (float)(rank + fill);
+        else ((int *)buffer)[i] = rank + fill;
     }
     void *d_buf = NULL, *d_res = NULL, *d_bar = NULL;
     CHECK_HIP(hipMalloc(&d_buf, bytes + 4));

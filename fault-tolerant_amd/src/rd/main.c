@@ -43,9 +43,12 @@ int main(int argc, char *argv[])
     size_t es = (dt == FTAR_FLOAT32) ? sizeof(float) : sizeof(int);
     void *buffer = malloc((size_t)buf_size * es + 1);
     void *result = malloc((size_t)buf_size * es + 1);
+    /* FTAR_FILL_OFFSET=k (default 0, the reference's input): buffer[i] = rank + k, so a one-rank
+     * run has a nonzero checksum, ((N(N-1)/2 + N k) % 17) * count */
+    const int fill = getenv("FTAR_FILL_OFFSET") ? atoi(getenv("FTAR_FILL_OFFSET")) : 0;
     for (int i = 0; i < buf_size; i++) {
-        if (dt == FTAR_FLOAT32) ((float *)buffer)[i] = (float)rank;
-        else ((int *)buffer)[i] = rank;
+        if (dt == FTAR_FLOAT32) ((float *)buffer)[i] = (float)(rank + fill);
+        else ((int *)buffer)[i] = rank + fill;
     }
     double t0 = now_s();
     ftar_recursive_doubling_host(buffer, result, (size_t)buf_size, dt, FTAR_SUM, comm);

@@ -69,7 +69,7 @@ def test_run_compare_campaign_hostsim(hostsim, tmp_path):
                FTAR_CMP_RD=f"{hs}/rd/main", FTAR_CMP_RABEN=f"{hs}/raben/main",
                FTAR_CMP_ORIG_RD=f"{hs}/rd/main", FTAR_CMP_ORIG_RABEN=f"{hs}/raben/main",
                FTAR_CMP_OUT=str(tmp_path / "out"), FTAR_CMP_DATA=str(tmp_path / "data"),
-               FTAR_HOSTSIM_TAG="compare")
+               FTAR_HOSTSIM_TAG="compare", FTAR_FILL_OFFSET="3")
     os.makedirs(tmp_path / "out")
     cp = subprocess.run(["./run_compare.sh", "1"], cwd=RUN, env=env, capture_output=True, text=True, timeout=300)
     subprocess.run("rm -f /dev/shm/ftarhs-compare-*", shell=True)
@@ -77,25 +77,27 @@ def test_run_compare_campaign_hostsim(hostsim, tmp_path):
     for name in ("rd", "original_rd", "raben", "original_raben"):
         rows = _rows(tmp_path / "data" / f"{name}.csv")
         assert len(rows) == 2 * 7, (name, rows)
-        for r in rows:
+        for r in rows:  # buffer[i] = rank + 3 (FTAR_FILL_OFFSET): the closed form with the offset
             n, size = int(r["NP"]), int(r["SIZE"])
-            assert int(r["RESULT"]) == ((n * (n - 1) // 2) % 17) * size
+            assert int(r["RESULT"]) == ((n * (n - 1) // 2 + 3 * n) % 17) * size
     assert not (tmp_path / "out" / "error.txt").exists()
 
 
 @pytest.mark.gpu
 def test_run_compare_campaign_gpu(tmp_path):
     """All four executables on the GPU (NP = 1: the box has one GPU and RCCL refuses two
-    ranks on one device), including the RCCL vendor baseline."""
+    ranks on one device), including the RCCL vendor baseline.  The inputs are rank + 5
+    (FTAR_FILL_OFFSET), so every RESULT is the nonzero closed form 5 * SIZE, not the 0 a
+    one-rank run of the reference's input gives whatever the drivers compute."""
     env = dict(os.environ, FTAR_CMP_NPS="1", FTAR_CMP_BUF_MIN="1", FTAR_CMP_BUF_MAX="256",
-               FTAR_CMP_OUT=str(tmp_path / "out"), FTAR_CMP_DATA=str(tmp_path / "data"))
+               FTAR_CMP_OUT=str(tmp_path / "out"), FTAR_CMP_DATA=str(tmp_path / "data"), FTAR_FILL_OFFSET="5")
     os.makedirs(tmp_path / "out")
     cp = subprocess.run(["./run_compare.sh", "1"], cwd=RUN, env=env, capture_output=True, text=True, timeout=600)
     assert cp.returncode == 0, cp.stdout[-2000:] + cp.stderr[-2000:]
     for name in ("rd", "original_rd", "raben", "original_raben"):
         rows = _rows(tmp_path / "data" / f"{name}.csv")
         assert len(rows) == 9, (name, rows, cp.stdout[-2000:])
-        assert all(int(r["RESULT"]) == 0 for r in rows)
+        assert all(int(r["RESULT"]) == 5 * int(r["SIZE"]) and int(r["SIZE"]) > 0 for r in rows), rows
 
 
 def _analyze():
