@@ -1257,6 +1257,8 @@ def multi(args):
     final["e2e_host_buffers"] = opt_leg("e2e_host_buffers", 20, e2e_leg)
     del xe, ye, want
 
+    # IPC exports the runtime refused and the library re-allocated (expected 0)
+    final["export_retries_max_over_ranks"] = int(max_over_ranks([float(comm.last_stats().export_retries)])[0])
     line = build_line(transports, t_ref, k_ref)
     line.update(final)
     line["c5_single_kill"] = c5

@@ -737,10 +737,11 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
     return FTAR_SUCCESS;
 }
 
-/* Pinned staging of the _host entry points, grown on demand.  Every rank of the comm
- * calls this at the start of the same collective, so a rank that cannot allocate ends the
- * job (MPI_Abort) instead of returning alone while its peers wait in the collective's
- * first barrier. */
+/* Pinned staging of the _host entry points, grown on demand.  Rank-local: whether a call
+ * stages at all is decided per rank (a rank whose caller buffers are pinned runs the
+ * device entry point on them in place and never gets here), so this does no collective
+ * work.  A rank that cannot allocate ends the job (MPI_Abort) rather than returning alone
+ * while its peers wait for it in the collective's first barrier. */
 int ftar_ensure_staging(ftar_comm *c, size_t bytes)
 {
     if (bytes == 0 || (bytes <= c->hbytes && c->hsend && c->hrecv)) return FTAR_SUCCESS;

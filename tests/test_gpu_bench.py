@@ -38,7 +38,7 @@ def test_bench_single_gpu_line():
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 10 and d["roofline"]["bound"] == "hbm"
     # within 10 % of the committed profile's fraction (the kernel sits at ~0.82 of 8 TB/s)
-    with open(os.path.join(ROOT, "profiles", "r03", "bench_n1_early.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r03", "bench_n1.json")) as f:
         committed = json.loads([l for l in f.read().splitlines() if l.startswith("{")][-1])["roofline"]["frac"]
     assert abs(d["roofline"]["frac"] - committed) <= 0.10 * committed, (d["roofline"], committed)
     assert "rotating" in d["config"]["buffers"]
