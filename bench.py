@@ -828,10 +828,11 @@ def multi(args):
     def quick(fn, steps=3, warmup=1):
         return timed(fn, steps, warmup)[0]
 
-    opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY, ftar.OPT_MESH)
+    opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY, ftar.OPT_MESH, ftar.OPT_PUSH)
     defaults = {o: comm.get_option(o) for o in opts}
 
     def set_opts(vals):
+        vals = tuple(vals) + (0,) * (len(opts) - len(vals))  # PUSH off unless named
         for o, v in zip(opts, vals):
             comm.set_option(o, v)
 
@@ -871,17 +872,22 @@ def multi(args):
     selection = None
     pow2 = world & (world - 1) == 0
     if world >= 2 and not args.no_variants:
+        # (mesh, relay, push): the mesh pulls the peers' parts of each block (remote loads)
+        # or, mesh_push, has every rank store its parts into the owners (remote stores) --
+        # which one the fabric moves faster is measured here, not assumed
         cands = {}
         if pow2 and comm.get_option(ftar.OPT_MESH):
-            cands["mesh"] = (1, 1)
+            cands["mesh"] = (1, 1, 0)
+            cands["mesh_push"] = (1, 1, 1)
         if world >= 3 and comm.get_option(ftar.OPT_RELAY):
-            cands["relay2hop"] = (0, 1)
-        cands["direct"] = (0, 0)
+            cands["relay2hop"] = (0, 1, 0)
+        cands["direct"] = (0, 0, 0)
         if len(cands) > 1:
             times, inexact, failed = {}, [], {}
-            for name, (m, r) in cands.items():
+            for name, (m, r, pu) in cands.items():
                 comm.set_option(ftar.OPT_MESH, m)
                 comm.set_option(ftar.OPT_RELAY, r)
+                comm.set_option(ftar.OPT_PUSH, pu)
                 try:
                     maybe_fail(f"select:{name}")
                     if max_over_ranks([exact_ok(comm.allreduce_rabenseifner, trials=(0,))])[0]:
@@ -892,12 +898,12 @@ def multi(args):
                     failed[name] = str(e)[-200:]
             if times:
                 chosen = min(times, key=times.get)
-                comm.set_option(ftar.OPT_MESH, cands[chosen][0])
-                comm.set_option(ftar.OPT_RELAY, cands[chosen][1])
+                for o, v in zip((ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH), cands[chosen]):
+                    comm.set_option(o, v)
             else:  # every one failed: keep the defaults, exact_on_node reports it
                 chosen = None
-                comm.set_option(ftar.OPT_MESH, defaults[ftar.OPT_MESH])
-                comm.set_option(ftar.OPT_RELAY, defaults[ftar.OPT_RELAY])
+                for o in (ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH):
+                    comm.set_option(o, defaults[o])
             selection = {f"{k}_ms": round(t * 1e3, 4) for k, t in times.items()}
             selection.update({"chosen": chosen, "inexact": inexact, "failed": failed})
 
@@ -908,7 +914,9 @@ def multi(args):
     relayed = comm.last_stats().relayed_steps > 0
     meshed = comm.last_stats().mesh_steps > 0
     oneshot = comm.last_stats().mesh_steps == 1  # the mesh's one-launch form (p = 2, small vectors)
-    transport = "mesh-oneshot" if oneshot else "mesh" if meshed else "relay2hop" if relayed else "direct"
+    pushed = meshed and not oneshot and comm.get_option(ftar.OPT_PUSH) != 0
+    transport = "mesh-oneshot" if oneshot else "mesh-push" if pushed else "mesh" if meshed else \
+        "relay2hop" if relayed else "direct"
     chosen_opts = {o: comm.get_option(o) for o in opts}
 
     L = world.bit_length() - 1
@@ -964,6 +972,9 @@ def multi(args):
                         "(power-of-two p, no spare)",
         "mesh": "Rabenseifner, one-hop mesh: reduce-scatter as one tree kernel over p-1 peer pulls, allgather as "
                 "one multi-source pull (power-of-two p, no spare; same reduction tree as recursive halving)",
+        "mesh-push": "Rabenseifner, one-hop mesh, push form: every rank stores its part of each block into the "
+                     "owner's HBM (p-1 remote-store copies in one launch), each owner reduces its block locally in the "
+                     "same tree, allgather as one multi-source pull (power-of-two p, no spare)",
         "relay2hop": "Rabenseifner, step by step (recursive halving + doubling), each exchange striped over 2-hop "
                      "relays",
         "direct": "Rabenseifner, step by step (recursive halving + doubling), one pairwise pull per step",
@@ -1022,6 +1033,8 @@ def multi(args):
                                          "tree and allgather kernels within 0.02 % of their algorithmic bytes)",
                          "kernel": ("Raben one-shot mesh: tree_batch_kernel, every block in its owner's tree"
                                     if oneshot
+                                    else "Raben mesh reduce-scatter, push form: p-1 remote-store copies in one launch"
+                                    if pushed
                                     else "Raben mesh reduce-scatter: tree_kernel over p-1 one-hop pulls" if meshed
                                     else "Raben RS step 0, both relay phases (stripes pulled over r-1 links)" if relayed
                                     else "Raben RS step 0 reduce half (pull partner's half, reduce into W)"),
@@ -1092,8 +1105,9 @@ def multi(args):
                   ("chosen_64KiB", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, 16384)]
         if not args.no_variants:
             checks += [(name, vals, comm.allreduce_rabenseifner, None) for name, vals in
-                       (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
-                        ("copy_engine", (0, 1, 1, 0, 0))) if pow2 or name != "mesh"]
+                       (("mesh", (1, 1, 0, 0, 1)), ("mesh_push", (1, 1, 0, 0, 1, 1)), ("relay2hop", (1, 1, 0, 0, 0)),
+                        ("direct", (0, 1, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)))
+                       if pow2 or not name.startswith("mesh")]
             checks += [("rd_relay", (1, 1, 0, 0, 0), comm.recursive_doubling, None),
                        ("rd_direct", (0, 1, 0, 0, 0), comm.recursive_doubling, None)]
         comm.set_profiling(False)
@@ -1159,12 +1173,12 @@ def multi(args):
         # the partner's window + a local reduce kernel; relay_full_exchange: the relay with
         # the reference's step-0 full exchange.  Each variant records its own failure.
         out = {}
-        variants = (("mesh", (1, 1, 0, 0, 1)), ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)),
-                    ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
+        variants = (("mesh", (1, 1, 0, 0, 1)), ("mesh_push", (1, 1, 0, 0, 1, 1)), ("relay2hop", (1, 1, 0, 0, 0)),
+                    ("direct", (0, 1, 0, 0, 0)), ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
                     ("relay_full_exchange", (1, 1, 0, 1, 0)))
         try:
             for name, vals in variants:
-                if name == "mesh" and not pow2:
+                if name.startswith("mesh") and not pow2:
                     continue
                 if time_left() < 10:
                     out[name] = {"skipped": "budget"}

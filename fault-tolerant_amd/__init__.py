@@ -27,6 +27,7 @@ PH_PRE, PH_LOOP, PH_AG, PH_POST = 0, 1, 2, 3
 PT_BEFORE, PT_AFTER, PT_BARRIER, PT_DURING = 0, 1, 2, 3
 OPT_OVERLAP, OPT_RELAY, OPT_RELAY_MIN, OPT_LOOP_SECONDS, OPT_COPY_ENGINE, OPT_REDUNDANCY, OPT_MESH = 0, 1, 2, 3, 4, 5, 6
 OPT_ONESHOT_MAX = 7
+OPT_PUSH = 8
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
 ERR_OP = 9  # MPI_ERR_OP: a logical / bitwise op on a float type
 

@@ -157,6 +157,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 0;
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
+    c->push = getenv("FTAR_PUSH") ? atoi(getenv("FTAR_PUSH")) : 0;
     c->oneshot_max = getenv("FTAR_ONESHOT_MAX") ? (size_t)atoll(getenv("FTAR_ONESHOT_MAX")) : ((size_t)1 << 20);
     c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
     c->stage_max = getenv("FTAR_STAGE_MAX") ? (size_t)atoll(getenv("FTAR_STAGE_MAX")) : ((size_t)1 << 20);
@@ -433,6 +434,7 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_REDUNDANCY: c->redundancy = v != 0; break;
     case FTAR_OPT_MESH: c->mesh = v != 0; break;
     case FTAR_OPT_ONESHOT_MAX: c->oneshot_max = (size_t)v; break;
+    case FTAR_OPT_PUSH: c->push = v != 0; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;
@@ -450,6 +452,7 @@ int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
     case FTAR_OPT_REDUNDANCY: *v = c->redundancy; break;
     case FTAR_OPT_MESH: *v = c->mesh; break;
     case FTAR_OPT_ONESHOT_MAX: *v = (double)c->oneshot_max; break;
+    case FTAR_OPT_PUSH: *v = c->push; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;
@@ -560,12 +563,16 @@ static void note_segs(ftar_comm *c, int dtype, const fdev_seg *segs, int nseg)
 {
     const void *remote = NULL;
     size_t bytes = 0;
+    int push = 0;
     for (int i = 0; i < nseg && !remote; i++) {
         if (segs[i].remote & FDEV_REMOTE_X) remote = segs[i].x;
         else if (segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) remote = segs[i].y;
+        push |= (segs[i].remote & FDEV_REMOTE_OUT) != 0;
         bytes = segs[i].n * ftar_esize(dtype);
     }
     ftar_note_launch(c, remote, bytes);
+    if (push && !remote) /* stores into peers' HBM: an exchange in flight too (nothing to re-pull) */
+        atomic_store_explicit(&c->job.shm->slot[c->wrank].inflight, FTAR_INFLIGHT_PULL, memory_order_release);
 }
 
 int ftar_drain(ftar_comm *c)

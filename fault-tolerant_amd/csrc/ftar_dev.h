@@ -29,6 +29,7 @@ extern "C" {
 
 #define FDEV_REMOTE_X 1
 #define FDEV_REMOTE_Y 2
+#define FDEV_REMOTE_OUT 4 /* `out` is a peer mapping (a push: remote stores) */
 
 typedef struct {
     int kind;

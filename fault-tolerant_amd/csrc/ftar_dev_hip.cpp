@@ -451,8 +451,9 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
         int nread = segs[i].kind == FDEV_COPY ? 1 : 2;
         int nremote = ((segs[i].remote & FDEV_REMOTE_X) ? 1 : 0) +
                       ((segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) ? 1 : 0);
-        d->ctr.link_bytes += b * nremote;
-        d->ctr.hbm_bytes += b * (1 + nread - nremote + (segs[i].out2 ? 1 : 0));
+        int rout = (segs[i].remote & FDEV_REMOTE_OUT) ? 1 : 0;
+        d->ctr.link_bytes += b * (nremote + rout);
+        d->ctr.hbm_bytes += b * (1 - rout + nread - nremote + (segs[i].out2 ? 1 : 0));
     }
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);

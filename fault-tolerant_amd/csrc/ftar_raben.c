@@ -49,6 +49,8 @@ typedef struct {
     int fast_io;    /* power of two, no recovery data: sbuf/rbuf used in place (see below) */
     int out_done;   /* the last allgather step already stored this rank's result in rbuf */
     int mesh;       /* fast_io on the full mesh: one-hop reduce-scatter and allgather */
+    int push;       /* the mesh's reduce-scatter by remote stores into the owners' R (FTAR_OPT_PUSH) */
+    int64_t slot;   /* push: elements per source slot in an owner's R */
     int oneshot;    /* mesh of a small vector: every block in its owner's tree, one launch */
     int in0_w[FTAR_MAX_RANKS]; /* world rank whose IN held vrank v's input at RS step 0 */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
@@ -277,6 +279,82 @@ static void rb_handler_ag(rb_ctx *x, uint64_t newf, int fs)
     c->stats.recoveries++;
 }
 
+/* Push form of the mesh (FTAR_OPT_PUSH): where the pull form's tree kernel reads the p - 1
+ * peers' parts of this rank's block over xGMI, here every rank stores its part of each
+ * peer's block INTO that peer (the owner's R, one slot per source) and each owner reduces
+ * its block from local memory.  Link bytes are the same (S/p per link and direction); the
+ * fabric moves remote stores instead of remote loads, which bench.py compares on the node.
+ * Slot j of owner u holds x_(u^j) over u's final block -- the tree's src[j] -- starting at
+ * the same element offset modulo 16 bytes as the block itself, so the copies and the tree
+ * keep their 16-byte vector bodies.  Returns the slot stride in elements, or 0 if the p - 1
+ * slots do not fit the workspace (the caller then pulls). */
+static int64_t rb_push_slot(const rb_ctx *x)
+{
+    int64_t e16 = (int64_t)(16 / x->es), bmax = 0;
+    for (int u = 0; u < x->adjsize; u++) {
+        int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
+        rb_windows(u, x->count, x->steps, ri, si, rc, sc);
+        if (rc[x->steps - 1] > bmax) bmax = rc[x->steps - 1];
+    }
+    int64_t stride = (bmax + e16 + 63) / 64 * 64; /* 256-byte multiples (x 4 or 8 B) */
+    if ((size_t)((x->adjsize - 1) * stride) * x->es > x->c->ws_bytes) return 0;
+    return stride;
+}
+
+static void *rb_push_at(const rb_ctx *x, void *R, int j, int64_t block_off)
+{
+    int64_t e16 = (int64_t)(16 / x->es);
+    return at(x, R, (int64_t)(j - 1) * x->slot + block_off % e16);
+}
+
+/* The reduce-scatter of rb_mesh in push form (see rb_push_slot): one launch of p - 1 remote
+ * copies, the phase's agree (every slot has landed), the owner's tree over local memory,
+ * and one more agree before the allgather reads the owners' blocks.  Kill points and
+ * outcomes are rb_mesh's (no idle rank: every failure aborts). */
+static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf)
+{
+    ftar_comm *c = x->c;
+    const int L = x->steps, p = x->adjsize, v = x->vrank;
+    void *W = c->ws[WS_W];
+    int64_t own0 = x->rindex[L - 1], own_n = x->rcount[L - 1];
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BEFORE);
+    ftar_enter(c);
+    fdev_seg segs[FDEV_MAX_SEGS];
+    int ns = 0;
+    for (int j = 1; j < p; j++) { /* owner u = v ^ j: its tree takes x_v as src[j] */
+        int u = v ^ j;
+        int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
+        rb_windows(u, x->count, L, ri, si, rc, sc);
+        void *R = ftar_buf(c, c->order[rb_real(x, u)], WS_R);
+        segs[ns++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_OUT, rb_push_at(x, R, j, ri[L - 1]),
+                                at(x, (void *)sbuf, ri[L - 1]), NULL, (size_t)rc[L - 1], NULL};
+    }
+    double lb0 = ftar_link_bytes(c);
+    ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP0);
+    ftar_launched(c, FTAR_PH_LOOP, 0); /* every step's DURING point: the pushes are in flight */
+    for (int s = 1; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_DURING);
+    ftar_drain(c);
+    ftar_exchange_done(c);
+    c->stats.step0_link_bytes += ftar_link_bytes(c) - lb0;
+    c->stats.steps += L;
+    c->stats.mesh_steps++;
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_AFTER);
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BARRIER);
+    uint64_t newf = ftar_step_sync(c, 3); /* every slot landed (:258-265) */
+    if (newf) rb_handler_rs(x, newf, L - 1); /* no idle rank: aborts */
+    const void *src[FDEV_MAX_TREE];
+    src[0] = at(x, (void *)sbuf, own0);
+    for (int j = 1; j < p; j++) src[j] = rb_push_at(x, c->ws[WS_R], j, own0);
+    if (fdev_tree(c->dev, x->dtype, x->op, src, p, 0, at(x, W, own0), (size_t)own_n, FDEV_TAG_STEP)) {
+        fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    ftar_note_launch(c, NULL, 0);
+    ftar_drain(c);
+    newf = ftar_step_sync(c, 3); /* every owner's block is final before the allgather reads it */
+    if (newf) rb_handler_rs(x, newf, L - 1);
+}
+
 /* The tolerant region at power-of-two p without an idle rank, on the full xGMI mesh.
  *
  * Recursive halving leaves in vrank v's final block the value
@@ -302,6 +380,11 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
     void *W = c->ws[WS_W];
     int64_t own0 = x->rindex[L - 1], own_n = x->rcount[L - 1];
 
+    uint64_t newf;
+    if (x->push) {
+        rb_mesh_push_rs(x, sbuf);
+        goto allgather;
+    }
     /* reduce-scatter: T(v, L) over this rank's final block */
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BEFORE);
     ftar_enter(c);
@@ -328,9 +411,10 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
     c->stats.mesh_steps++;
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_AFTER);
     for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BARRIER);
-    uint64_t newf = ftar_step_sync(c, 2); /* agree + barrier (:258-265) */
+    newf = ftar_step_sync(c, 2); /* agree + barrier (:258-265) */
     if (newf) rb_handler_rs(x, newf, L - 1); /* no idle rank: aborts */
 
+allgather:
     /* allgather: every peer's final block into rbuf, this rank's own out of W */
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
     ftar_enter(c);
@@ -492,6 +576,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * link and pays off only below oneshot_max. */
     x->oneshot = x->mesh && c->size <= FDEV_MAX_BATCH && c->oneshot_max > 0 &&
                  (c->size == 2 || count * (size_t)x->es <= c->oneshot_max);
+    x->push = x->mesh && !x->oneshot && c->push;
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);
@@ -499,6 +584,10 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
 
     size_t bytes = count * x->es;
     ftar_ensure_workspace(c, bytes);
+    if (x->push) { /* uniform: the same geometry on every rank */
+        x->slot = rb_push_slot(x);
+        x->push = x->slot > 0;
+    }
     void *IN = c->ws[WS_IN], *W = c->ws[WS_W], *T = c->ws[WS_T];
     fdev_order_after(c->dev, c->user_stream); /* sbuf may still be in flight on the caller's stream */
     rb_vrank(x);
@@ -511,9 +600,14 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     int disjoint = s0 + bytes <= d0 || d0 + bytes <= s0;
     /* The one-shot launch writes rbuf while peers still read this rank's input: in place,
      * that input must be staged (whole: peers read every block of it). */
-    int aliased = ftar_stage_input(c, sbuf, bytes,
+    /* push: no peer ever reads this rank's input (it stores its parts into the owners) */
+    int aliased = x->push ? 0 :
+                  ftar_stage_input(c, sbuf, bytes,
                                    x->oneshot ? disjoint : (x->fast_io || (x->rank >= 2 * x->rem && disjoint)));
-    if (aliased) {
+    if (x->push) {
+        ftar_inputs_done(c);
+        rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
+    } else if (aliased) {
         IN = (void *)sbuf;
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
     } else if (x->oneshot) {

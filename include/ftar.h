@@ -197,8 +197,10 @@ typedef enum {
     FTAR_OPT_REDUNDANCY = 5,   /* Raben step-0 recovery copy: 0 only when a spare exists, 1 always */
     FTAR_OPT_MESH = 6,         /* Raben at power-of-two p without a spare: one-hop reduce-scatter and
                                   allgather over the full mesh, same reduction tree (0/1) */
-    FTAR_OPT_ONESHOT_MAX = 7   /* mesh Raben up to this many bytes per vector (any size at p = 2): one
+    FTAR_OPT_ONESHOT_MAX = 7,  /* mesh Raben up to this many bytes per vector (any size at p = 2): one
                                   launch computes every block in its owner's tree into rbuf (0 = off) */
+    FTAR_OPT_PUSH = 8          /* mesh Raben's reduce-scatter by remote stores: every rank writes its part
+                                  of each block into the owner's HBM, the owner reduces locally (0/1) */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);

@@ -222,6 +222,7 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
             }
         }
         if (s->out2) memmove(s->out2, s->out, s->n * esz(dtype));
+        if (s->remote & FDEV_REMOTE_OUT) d->ctr.link_bytes += (double)s->n * (double)esz(dtype);
     }
     d->ctr.launches[tag]++;
     return 0;

@@ -275,18 +275,21 @@ def test_torch_device_buffers(oracle, algo, p, mode):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
+@pytest.mark.parametrize("push", ["0", "1"])
 @pytest.mark.parametrize("p,op,count", [(2, 0, 100003), (4, 0, 100003), (8, 0, 65536 + 5), (4, 2, 4099), (8, 3, 4099),
                                         (4, 0, (1 << 22) + 13), (8, 1, (1 << 20) + 3)])
-def test_mesh_schedule(oracle, p, op, count):
-    """Power of two without a spare: one-hop reduce-scatter (tree kernel over p - 1
-    peer pulls) and allgather, bit-identical to the step-by-step schedule -- MAX/MIN with
-    NaN and signed zeros pin the operand order of every combination."""
+def test_mesh_schedule(oracle, p, op, count, push):
+    """Power of two without a spare: one-hop reduce-scatter -- a tree kernel over p - 1
+    peer pulls, or (FTAR_PUSH=1) p - 1 remote-store copies into the owners followed by the
+    owner's tree over local memory -- and allgather, bit-identical to the step-by-step
+    schedule; MAX/MIN with NaN and signed zeros pin the operand order of every combination."""
     dt = np.int32 if op == 1 else np.float32
     ins = oracle.random_inputs(p, count, seed=p * 7 + op, dtype=dt)
     if op >= 2:
         ins = H.with_specials(ins, p + op)
     # one device-resident call (the host pipeline would split >= 16 MiB into chunk calls)
-    o, r = _check(oracle.rabenseifner, "raben", ins, op=op, env={"FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0"})
+    o, r = _check(oracle.rabenseifner, "raben", ins, op=op,
+                  env={"FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0", "FTAR_PUSH": push})
     assert all(st[0][9] == 2 for st in r.status.values()), r.status
 
 
@@ -325,13 +328,14 @@ def test_oneshot_device_buffers(oracle, p, count, mode):
         assert np.array_equal(r.outputs[w][1].view(np.uint32), (sign * o.outputs[w]).view(np.uint32))
 
 
-@pytest.mark.parametrize("form", ["0", str(1 << 20)])
-@pytest.mark.parametrize("kill", [(3, 1, 1, 2), (0, 2, 0, 1), (5, 1, 0, 0)])
+@pytest.mark.parametrize("form", ["0", str(1 << 20), "push"])
+@pytest.mark.parametrize("kill", [(3, 1, 1, 2), (0, 2, 0, 1), (5, 1, 0, 0), (2, 1, 1, 3)])
 def test_mesh_kill_aborts(oracle, kill, form):
-    """Any death in the mesh phases (two-launch and one-shot) ends the job like the
-    reference at p = 8 (no idle rank)."""
-    _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, 10007, seed=kill[0]), [kill],
-           env={"FTAR_ONESHOT_MAX": form})
+    """Any death in the mesh phases (two-launch, one-shot, push) ends the job like the
+    reference at p = 8 (no idle rank); (2, 1, 1, 3) dies mid-exchange with its peers'
+    kernels reading (or, push, writing) its HBM."""
+    env = {"FTAR_ONESHOT_MAX": "0", "FTAR_PUSH": "1"} if form == "push" else {"FTAR_ONESHOT_MAX": form}
+    _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, 10007, seed=kill[0]), [kill], env=env)
 
 
 @pytest.mark.parametrize("p", [4, 8])

@@ -349,7 +349,12 @@ def test_device_entry_points(hostsim, oracle, algo, p, mode, relay):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
-ONESHOT = {"mesh": "0", "oneshot": str(1 << 20)}  # FTAR_ONESHOT_MAX
+ONESHOT = {"mesh": "0", "oneshot": str(1 << 20), "push": "0"}  # FTAR_ONESHOT_MAX
+
+
+def _form_env(form):
+    """The mesh's forms: two launches (pull), one-shot, and the push reduce-scatter."""
+    return {"FTAR_ONESHOT_MAX": ONESHOT[form], "FTAR_PUSH": "1" if form == "push" else "0"}
 
 
 def _mesh_launches(p, form):
@@ -366,8 +371,11 @@ def test_mesh_parity(hostsim, oracle, p, dtype, op, form):
     ins = oracle.random_inputs(p, 4099, seed=p * 10 + op, dtype=dtype)
     if op >= 2:
         ins = H.with_specials(ins, p + op)
-    o, r = _cmp(oracle.rabenseifner, "raben", ins, op=op, env={"FTAR_ONESHOT_MAX": ONESHOT[form]})
+    o, r = _cmp(oracle.rabenseifner, "raben", ins, op=op, env=_form_env(form))
     assert all(st[0][9] == _mesh_launches(p, form) for st in r.status.values()), r.status
+    if form == "push":  # the push form took its own path: one agree more than the pull form's
+        _, rp = _cmp(oracle.rabenseifner, "raben", ins, op=op, env=_form_env("mesh"))
+        assert all(r.status[w][0][7] == rp.status[w][0][7] + 1 for w in r.status), (r.status, rp.status)
 
 
 @pytest.mark.parametrize("form", sorted(ONESHOT))
@@ -376,7 +384,7 @@ def test_mesh_single_kill_sweep(hostsim, oracle, p, form):
     """Every kill point of every step lands in the collapsed phases: the job aborts
     exactly where the reference aborts (all of them, no idle rank)."""
     ins = oracle.random_inputs(p, 1031, seed=p + 500)
-    env = {"FTAR_ONESHOT_MAX": ONESHOT[form]}
+    env = _form_env(form)
     n = 0
     for v in range(p):
         for ph in (0, 1, 2, 3):
@@ -397,7 +405,7 @@ def test_mesh_tiny_counts(hostsim, oracle, p, n, form):
     """Vectors shorter than the rank count: empty final blocks on some ranks (in place:
     the one-shot form stages the input whole)."""
     o, r = _cmp(oracle.rabenseifner, "raben", oracle.random_inputs(p, n, seed=p + n),
-                env={"FTAR_PROBE_DEVICE": "1", "FTAR_PROBE_INPLACE": "1", "FTAR_ONESHOT_MAX": ONESHOT[form]})
+                env=dict(_form_env(form), FTAR_PROBE_DEVICE="1", FTAR_PROBE_INPLACE="1"))
     assert all(st[0][9] == _mesh_launches(p, form) for st in r.status.values())
 
 
