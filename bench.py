@@ -878,7 +878,9 @@ def multi(args):
         cands = {}
         if pow2 and comm.get_option(ftar.OPT_MESH):
             cands["mesh"] = (1, 1, 0)
-            cands["mesh_push"] = (1, 1, 1)
+            cands["mesh_push"] = (1, 1, 1)  # remote stores in the reduce-scatter
+            if world <= 8:
+                cands["mesh_push2"] = (1, 1, 2)  # ... and in the allgather
         if world >= 3 and comm.get_option(ftar.OPT_RELAY):
             cands["relay2hop"] = (0, 1, 0)
         cands["direct"] = (0, 0, 0)
@@ -914,9 +916,10 @@ def multi(args):
     relayed = comm.last_stats().relayed_steps > 0
     meshed = comm.last_stats().mesh_steps > 0
     oneshot = comm.last_stats().mesh_steps == 1  # the mesh's one-launch form (p = 2, small vectors)
-    pushed = meshed and not oneshot and comm.get_option(ftar.OPT_PUSH) != 0
-    transport = "mesh-oneshot" if oneshot else "mesh-push" if pushed else "mesh" if meshed else \
-        "relay2hop" if relayed else "direct"
+    push_opt = int(comm.get_option(ftar.OPT_PUSH))
+    pushed = meshed and not oneshot and push_opt != 0
+    transport = "mesh-oneshot" if oneshot else ("mesh-push2" if push_opt == 2 and world <= 8 else "mesh-push") \
+        if pushed else "mesh" if meshed else "relay2hop" if relayed else "direct"
     chosen_opts = {o: comm.get_option(o) for o in opts}
 
     L = world.bit_length() - 1
@@ -975,6 +978,9 @@ def multi(args):
         "mesh-push": "Rabenseifner, one-hop mesh, push form: every rank stores its part of each block into the "
                      "owner's HBM (p-1 remote-store copies in one launch), each owner reduces its block locally in the "
                      "same tree, allgather as one multi-source pull (power-of-two p, no spare)",
+        "mesh-push2": "Rabenseifner, one-hop mesh, push form in both phases: remote-store copies into the owners, the "
+                      "owner's tree stores its block into every peer's workspace and its own rbuf, one local copy "
+                      "of the peers' blocks to rbuf (power-of-two p <= 8, no spare)",
         "relay2hop": "Rabenseifner, step by step (recursive halving + doubling), each exchange striped over 2-hop "
                      "relays",
         "direct": "Rabenseifner, step by step (recursive halving + doubling), one pairwise pull per step",
@@ -1105,7 +1111,8 @@ def multi(args):
                   ("chosen_64KiB", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, 16384)]
         if not args.no_variants:
             checks += [(name, vals, comm.allreduce_rabenseifner, None) for name, vals in
-                       (("mesh", (1, 1, 0, 0, 1)), ("mesh_push", (1, 1, 0, 0, 1, 1)), ("relay2hop", (1, 1, 0, 0, 0)),
+                       (("mesh", (1, 1, 0, 0, 1)), ("mesh_push", (1, 1, 0, 0, 1, 1)),
+                        ("mesh_push2", (1, 1, 0, 0, 1, 2)), ("relay2hop", (1, 1, 0, 0, 0)),
                         ("direct", (0, 1, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)))
                        if pow2 or not name.startswith("mesh")]
             checks += [("rd_relay", (1, 1, 0, 0, 0), comm.recursive_doubling, None),
@@ -1173,7 +1180,8 @@ def multi(args):
         # the partner's window + a local reduce kernel; relay_full_exchange: the relay with
         # the reference's step-0 full exchange.  Each variant records its own failure.
         out = {}
-        variants = (("mesh", (1, 1, 0, 0, 1)), ("mesh_push", (1, 1, 0, 0, 1, 1)), ("relay2hop", (1, 1, 0, 0, 0)),
+        variants = (("mesh", (1, 1, 0, 0, 1)), ("mesh_push", (1, 1, 0, 0, 1, 1)), ("mesh_push2", (1, 1, 0, 0, 1, 2)),
+                    ("relay2hop", (1, 1, 0, 0, 0)),
                     ("direct", (0, 1, 0, 0, 0)), ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
                     ("relay_full_exchange", (1, 1, 0, 1, 0)))
         try:

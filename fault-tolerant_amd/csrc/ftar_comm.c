@@ -434,7 +434,7 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_REDUNDANCY: c->redundancy = v != 0; break;
     case FTAR_OPT_MESH: c->mesh = v != 0; break;
     case FTAR_OPT_ONESHOT_MAX: c->oneshot_max = (size_t)v; break;
-    case FTAR_OPT_PUSH: c->push = v != 0; break;
+    case FTAR_OPT_PUSH: c->push = v >= 2 ? 2 : v != 0; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;

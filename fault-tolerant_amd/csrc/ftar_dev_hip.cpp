@@ -478,15 +478,21 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
 int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
               size_t n, int tag)
 {
+    return fdev_tree_out(d, dtype, op, src, nsrc, remote_mask, out, nullptr, 0, n, tag);
+}
+
+int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
+                  void *const *more, int nmore, size_t n, int tag)
+{
     size_t es = esize_of(dtype);
     if (es == 0 || op < 0 || op >= ftar::kNumOps || tag < 0 || tag >= FDEV_NTAGS ||
-        !(nsrc == 2 || nsrc == 4 || nsrc == 8 || nsrc == 16)) {
+        !(nsrc == 2 || nsrc == 4 || nsrc == 8 || nsrc == 16) || nmore < 0 || nmore > ftar::kMaxMore) {
         snprintf(g_err, sizeof(g_err), "fdev_tree: bad arguments");
         return 13;
     }
     if (n == 0) return 0;
     int nremote = __builtin_popcount(remote_mask & ((1u << nsrc) - 1));
-    d->ctr.link_bytes += (double)n * (double)es * nremote;
+    d->ctr.link_bytes += (double)n * (double)es * (nremote + nmore); // extra destinations: peers' HBM
     d->ctr.hbm_bytes += (double)n * (double)es * (nsrc - nremote + 1);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
@@ -502,6 +508,8 @@ int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, 
         memset(&A, 0, sizeof(A));
         for (int j = 0; j < nsrc; j++) A.src[j] = (const char *)src[j] + off * es;
         A.out = (char *)out + off * es;
+        A.nmore = nmore;
+        for (int o = 0; o < nmore; o++) A.more[o] = (char *)more[o] + off * es;
         A.n = n - off < piece ? n - off : piece;
         A.nt_store = nt_store();
         unsigned grid = ftar::plan_tree(&A, nsrc, es, d->max_blocks + 1);

@@ -84,7 +84,7 @@ struct ftar_comm {
     int copy_engine;     /* FTAR_COPY_ENGINE (default 0): direct pulls by hipMemcpyAsync */
     int redundancy;      /* FTAR_REDUNDANCY (default 0: the step-0 copy is never moved; a replay reads the dead rank's IN) */
     int mesh;            /* FTAR_MESH (default 1): one-hop Raben at power-of-two p without a spare */
-    int push;            /* FTAR_PUSH (default 0): the mesh's reduce-scatter by remote stores */
+    int push;            /* FTAR_PUSH (default 0): the mesh by remote stores -- 1 reduce-scatter, 2 both phases */
     size_t oneshot_max;  /* FTAR_ONESHOT_MAX bytes: mesh Raben in one launch up to this size */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
     /* the step's last peer read (FTAR_LOOP_SECONDS re-pulls it into pad while it waits) */

@@ -103,9 +103,12 @@ struct SegIn {
 // (src[j] = vrank owner ^ j) this is exactly the value recursive halving leaves in the
 // owner's final block (every level: the owner's subtree first).
 constexpr int kMaxTree = 16;
+constexpr int kMaxMore = 7; // extra destinations of one tree (the push mesh's allgather: every peer)
 struct TreeArgs {
     const void *src[kMaxTree];
     void *out;
+    void *more[kMaxMore]; // further destinations receiving the same values (nmore of them)
+    int nmore;
     size_t n;      // elements
     size_t head;   // scalar elements before the 16-byte vector body (co-aligned sources)
     size_t nv;     // 16-byte vectors in the body (0 when the pointers are not co-aligned)

@@ -282,6 +282,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs &A, unsigned b, unsigne
 #pragma unroll
             for (int j = 0; j < P; j += 2 * w) v[j] = apply16<T, OP>(v[j], v[j + w]);
         st16((uint4 *)((T *)A.out + A.head) + i, v[0], A.nt_store);
+        for (int o = 0; o < A.nmore; o++) st16((uint4 *)((T *)A.more[o] + A.head) + i, v[0], A.nt_store);
         return;
     }
     constexpr size_t E = 16 / sizeof(T);
@@ -298,6 +299,7 @@ __device__ __forceinline__ void tree_body(const TreeArgs &A, unsigned b, unsigne
 #pragma unroll
             for (int j = 0; j < P; j += 2 * w) v[j] = apply<T, OP>(v[j], v[j + w]);
         ((T *)A.out)[e] = v[0];
+        for (int o = 0; o < A.nmore; o++) ((T *)A.more[o])[e] = v[0];
     }
 }
 
@@ -328,6 +330,7 @@ unsigned plan_tree(TreeArgs *A, int p, size_t esize, unsigned max_blocks)
     uintptr_t mis = (uintptr_t)A->out & 15;
     bool co = (16 % esize == 0) && (mis % esize == 0);
     for (int j = 0; j < p; j++) co = co && (((uintptr_t)A->src[j] & 15) == mis);
+    for (int o = 0; o < A->nmore; o++) co = co && (((uintptr_t)A->more[o] & 15) == mis);
     A->head = A->nv = 0;
     if (co) {
         size_t head = mis ? (16 - mis) / esize : 0;

@@ -311,7 +311,7 @@ static void *rb_push_at(const rb_ctx *x, void *R, int j, int64_t block_off)
  * copies, the phase's agree (every slot has landed), the owner's tree over local memory,
  * and one more agree before the allgather reads the owners' blocks.  Kill points and
  * outcomes are rb_mesh's (no idle rank: every failure aborts). */
-static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf)
+static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf, void *rbuf)
 {
     ftar_comm *c = x->c;
     const int L = x->steps, p = x->adjsize, v = x->vrank;
@@ -345,14 +345,65 @@ static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf)
     const void *src[FDEV_MAX_TREE];
     src[0] = at(x, (void *)sbuf, own0);
     for (int j = 1; j < p; j++) src[j] = rb_push_at(x, c->ws[WS_R], j, own0);
-    if (fdev_tree(c->dev, x->dtype, x->op, src, p, 0, at(x, W, own0), (size_t)own_n, FDEV_TAG_STEP)) {
+    /* push == 2: the allgather rides on the tree -- its result goes to this rank's rbuf
+     * and straight into every peer's W (the owner's block, remote stores) */
+    void *more[FDEV_MAX_TREE];
+    int nmore = 0;
+    if (x->push == 2) {
+        for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
+        ftar_enter(c);
+        for (int j = 1; j < p; j++) more[nmore++] = at(x, ftar_buf(c, c->order[rb_real(x, v ^ j)], WS_W), own0);
+    }
+    void *out = x->push == 2 ? at(x, rbuf, own0) : at(x, W, own0);
+    if (fdev_tree_out(c->dev, x->dtype, x->op, src, p, 0, out, more, nmore, (size_t)own_n, FDEV_TAG_STEP)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
-    ftar_note_launch(c, NULL, 0);
+    ftar_note_launch(c, nmore ? more[0] : NULL, 0);
+    if (x->push == 2) {
+        ftar_launched(c, FTAR_PH_AG, L - 1);
+        for (int s = L - 2; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_DURING);
+    }
     ftar_drain(c);
-    newf = ftar_step_sync(c, 3); /* every owner's block is final before the allgather reads it */
+    if (x->push == 2) {
+        ftar_exchange_done(c);
+        c->stats.steps += L;
+        c->stats.mesh_steps++;
+        for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_AFTER);
+        for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BARRIER);
+    }
+    /* every owner's block is final (push == 1: before the allgather pulls it; push == 2:
+     * every peer's pushed block has landed in this rank's W) */
+    newf = ftar_step_sync(c, 3);
     if (newf) rb_handler_rs(x, newf, L - 1);
+}
+
+/* push == 2, after rb_mesh_push_rs: the peers' blocks, pushed into this rank's W, to rbuf
+ * (one local copy launch), then the ERRORS_ARE_FATAL barrier (:357-360).  The copy comes
+ * before this rank arrives at the barrier: no peer's next call can push into W while it
+ * is being read. */
+static int rb_mesh_push_finish(rb_ctx *x, void *rbuf)
+{
+    ftar_comm *c = x->c;
+    const int L = x->steps, p = x->adjsize, v = x->vrank;
+    fdev_seg segs[FDEV_MAX_SEGS];
+    int ns = 0;
+    for (int j = 1; j < p; j++) {
+        int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
+        rb_windows(v ^ j, x->count, L, ri, si, rc, sc);
+        segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, ri[L - 1]), at(x, c->ws[WS_W], ri[L - 1]), NULL,
+                                (size_t)rc[L - 1], NULL};
+    }
+    ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_LOCAL);
+    ftar_drain(c);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
+    uint64_t newf = ftar_step_sync(c, 3);
+    if (newf) rb_handler_ag(x, newf, 0); /* no idle rank: aborts */
+    ftar_stats_end(c);
+    return FTAR_SUCCESS;
 }
 
 /* The tolerant region at power-of-two p without an idle rank, on the full xGMI mesh.
@@ -382,7 +433,8 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
 
     uint64_t newf;
     if (x->push) {
-        rb_mesh_push_rs(x, sbuf);
+        rb_mesh_push_rs(x, sbuf, rbuf);
+        if (x->push == 2) return rb_mesh_push_finish(x, rbuf);
         goto allgather;
     }
     /* reduce-scatter: T(v, L) over this rank's final block */
@@ -576,7 +628,8 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * link and pays off only below oneshot_max. */
     x->oneshot = x->mesh && c->size <= FDEV_MAX_BATCH && c->oneshot_max > 0 &&
                  (c->size == 2 || count * (size_t)x->es <= c->oneshot_max);
-    x->push = x->mesh && !x->oneshot && c->push;
+    /* push 2 (both phases) needs every peer as an extra destination of one tree: p <= 8 */
+    x->push = (x->mesh && !x->oneshot && c->push) ? (c->push == 2 && c->size <= 8 ? 2 : 1) : 0;
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);

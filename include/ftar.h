@@ -199,8 +199,10 @@ typedef enum {
                                   allgather over the full mesh, same reduction tree (0/1) */
     FTAR_OPT_ONESHOT_MAX = 7,  /* mesh Raben up to this many bytes per vector (any size at p = 2): one
                                   launch computes every block in its owner's tree into rbuf (0 = off) */
-    FTAR_OPT_PUSH = 8          /* mesh Raben's reduce-scatter by remote stores: every rank writes its part
-                                  of each block into the owner's HBM, the owner reduces locally (0/1) */
+    FTAR_OPT_PUSH = 8          /* mesh Raben by remote stores: 1 = reduce-scatter (every rank writes its part
+                                  of each block into the owner's HBM, the owner reduces locally), 2 = both
+                                  phases (the owner's tree also stores its block into every peer; p <= 8),
+                                  0 = remote loads (default) */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);

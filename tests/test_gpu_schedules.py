@@ -264,6 +264,7 @@ def test_torch_device_buffers(oracle, algo, p, mode):
     the Python package: in place, at element offsets, two calls; sbuf untouched."""
     env = {"plain": {}, "inplace": {"FTAR_PROBE_INPLACE": "1"}, "offset1": {"FTAR_PROBE_OFFSET": "1"},
            "inplace_offset3": {"FTAR_PROBE_INPLACE": "1", "FTAR_PROBE_OFFSET": "3"}}[mode]
+    env = dict(env, FTAR_STAGE_MAX="0")  # peers read sbuf in place (the path above 1 MiB)
     ins = oracle.random_inputs(p, 65536 + 17, seed=p + 90)
     o = (oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling)(ins)
     r = H.run_torch_worker(algo, ins, devmap=ALL_ON_GPU0, env_extra=env)
@@ -275,14 +276,15 @@ def test_torch_device_buffers(oracle, algo, p, mode):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
-@pytest.mark.parametrize("push", ["0", "1"])
+@pytest.mark.parametrize("push", ["0", "1", "2"])
 @pytest.mark.parametrize("p,op,count", [(2, 0, 100003), (4, 0, 100003), (8, 0, 65536 + 5), (4, 2, 4099), (8, 3, 4099),
                                         (4, 0, (1 << 22) + 13), (8, 1, (1 << 20) + 3)])
 def test_mesh_schedule(oracle, p, op, count, push):
     """Power of two without a spare: one-hop reduce-scatter -- a tree kernel over p - 1
     peer pulls, or (FTAR_PUSH=1) p - 1 remote-store copies into the owners followed by the
-    owner's tree over local memory -- and allgather, bit-identical to the step-by-step
-    schedule; MAX/MIN with NaN and signed zeros pin the operand order of every combination."""
+    owner's tree over local memory -- and allgather (FTAR_PUSH=2: the owner's tree also
+    stores its block into every peer), bit-identical to the step-by-step schedule; MAX/MIN
+    with NaN and signed zeros pin the operand order of every combination."""
     dt = np.int32 if op == 1 else np.float32
     ins = oracle.random_inputs(p, count, seed=p * 7 + op, dtype=dt)
     if op >= 2:
@@ -319,7 +321,8 @@ def test_oneshot_device_buffers(oracle, p, count, mode):
     sbuf == rbuf), misaligned offsets, a re-allocated sbuf; sbuf never written."""
     ins = oracle.random_inputs(p, count, seed=p + count)
     o = oracle.rabenseifner(ins)
-    r = H.run_torch_worker("raben", ins, devmap=ALL_ON_GPU0, env_extra=dict(mode, FTAR_ONESHOT_MAX=str(1 << 20)))
+    r = H.run_torch_worker("raben", ins, devmap=ALL_ON_GPU0,
+                           env_extra=dict(mode, FTAR_ONESHOT_MAX=str(1 << 20), FTAR_STAGE_MAX="0"))
     assert r.returncode == 0, r.stderr[-2000:]
     sign = -1 if mode.get("FTAR_PROBE_REALLOC") else 1
     for w in range(p):
@@ -328,13 +331,14 @@ def test_oneshot_device_buffers(oracle, p, count, mode):
         assert np.array_equal(r.outputs[w][1].view(np.uint32), (sign * o.outputs[w]).view(np.uint32))
 
 
-@pytest.mark.parametrize("form", ["0", str(1 << 20), "push"])
+@pytest.mark.parametrize("form", ["0", str(1 << 20), "push", "push2"])
 @pytest.mark.parametrize("kill", [(3, 1, 1, 2), (0, 2, 0, 1), (5, 1, 0, 0), (2, 1, 1, 3)])
 def test_mesh_kill_aborts(oracle, kill, form):
     """Any death in the mesh phases (two-launch, one-shot, push) ends the job like the
     reference at p = 8 (no idle rank); (2, 1, 1, 3) dies mid-exchange with its peers'
     kernels reading (or, push, writing) its HBM."""
-    env = {"FTAR_ONESHOT_MAX": "0", "FTAR_PUSH": "1"} if form == "push" else {"FTAR_ONESHOT_MAX": form}
+    env = {"FTAR_ONESHOT_MAX": "0", "FTAR_PUSH": "2" if form == "push2" else "1"} if form.startswith("push") \
+        else {"FTAR_ONESHOT_MAX": form}
     _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, 10007, seed=kill[0]), [kill], env=env)
 
 

@@ -349,12 +349,13 @@ def test_device_entry_points(hostsim, oracle, algo, p, mode, relay):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
-ONESHOT = {"mesh": "0", "oneshot": str(1 << 20), "push": "0"}  # FTAR_ONESHOT_MAX
+ONESHOT = {"mesh": "0", "oneshot": str(1 << 20), "push": "0", "push2": "0"}  # FTAR_ONESHOT_MAX
 
 
 def _form_env(form):
-    """The mesh's forms: two launches (pull), one-shot, and the push reduce-scatter."""
-    return {"FTAR_ONESHOT_MAX": ONESHOT[form], "FTAR_PUSH": "1" if form == "push" else "0"}
+    """The mesh's forms: two launches (pull), one-shot, the push reduce-scatter, and push in
+    both phases (the owner's tree also stores its block into every peer)."""
+    return {"FTAR_ONESHOT_MAX": ONESHOT[form], "FTAR_PUSH": {"push": "1", "push2": "2"}.get(form, "0")}
 
 
 def _mesh_launches(p, form):
@@ -373,7 +374,7 @@ def test_mesh_parity(hostsim, oracle, p, dtype, op, form):
         ins = H.with_specials(ins, p + op)
     o, r = _cmp(oracle.rabenseifner, "raben", ins, op=op, env=_form_env(form))
     assert all(st[0][9] == _mesh_launches(p, form) for st in r.status.values()), r.status
-    if form == "push":  # the push form took its own path: one agree more than the pull form's
+    if form.startswith("push"):  # the push forms take their own path: one agree more than the pull form's
         _, rp = _cmp(oracle.rabenseifner, "raben", ins, op=op, env=_form_env("mesh"))
         assert all(r.status[w][0][7] == rp.status[w][0][7] + 1 for w in r.status), (r.status, rp.status)
 
@@ -444,7 +445,7 @@ def test_peer_input_map_failure_falls_back(hostsim, oracle, algo, p):
     ins = oracle.random_inputs(p, 5003, seed=p + 950)
     o = _fn(oracle, algo)(ins)
     r = H.run_probe(algo, ins, iters=2, backend="hostsim",
-                    env_extra={"FTAR_HOSTSIM_FAIL_IMPORT": str(4 * (p - 1) + 1)})
+                    env_extra={"FTAR_HOSTSIM_FAIL_IMPORT": str(4 * (p - 1) + 1), "FTAR_STAGE_MAX": "0"})
     assert r.returncode == 0, r.stderr[-2000:]
     assert "inputs are staged from now on" in r.stderr
     for w in range(p):
