@@ -1209,7 +1209,7 @@ def multi(args):
         return out
 
     def sweep_leg():
-        # Per-call time over message sizes (max over ranks), 4 B .. 256 MiB, with the chosen
+        # Per-call time over message sizes (max over ranks), 4 B .. 512 MiB, with the chosen
         # transport, next to RCCL's all_reduce on the same sizes: the FT/vendor curve of the
         # reference's compare campaign (slurm/test_compare.slurm:27-50, check_compare.py),
         # plus the fixed cost per call and the one-shot threshold (FTAR_ONESHOT_MAX)
@@ -1248,6 +1248,26 @@ def multi(args):
                     row["raben_over_rccl"] = round(row["raben_us"] / row["rccl_us"], 3)
                 sizes[str(4 * n)] = row
                 n *= 2
+            if n == 2 * args.count and "truncated_at_bytes" not in sizes:
+                # the reference's campaign ends at 2^27 ints = 512 MiB (run/run_compare.sh): one
+                # more point on a vector twice the job's, allocated for it and freed after
+                if time_left() < 20:
+                    sizes["truncated_at_bytes"] = 4 * n
+                else:
+                    xb = torch.cat([x, x])
+                    yb = torch.empty_like(xb)
+                    row = {"bytes": 4 * n}
+                    for name, fn in (("raben", comm.allreduce_rabenseifner), ("rd", comm.recursive_doubling)):
+                        def call(fn=fn):
+                            if fn(xb, yb) != 0:
+                                raise CallFailed(f"size sweep call of {4 * n} B failed")
+
+                        row[name + "_us"] = round(quick(call, steps=5, warmup=2) * 1e6, 2)
+                    if z is not None:
+                        row["rccl_us"] = round(quick(lambda: dist.all_reduce(xb), steps=5, warmup=2) * 1e6, 2)
+                        row["raben_over_rccl"] = round(row["raben_us"] / row["rccl_us"], 3)
+                    sizes[str(4 * n)] = row
+                    del xb, yb
         finally:
             comm.set_profiling(True)
         return sizes

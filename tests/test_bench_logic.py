@@ -262,6 +262,9 @@ def test_bench_multi_headline_survives_hung_and_failing_legs(hostsim, tmp_path):
     assert fin["exact_on_node"]["all_exact"], fin["exact_on_node"]
     assert fin["int32_rank_checksum_ok"] == {"raben": True, "rd": True}
     assert fin["cpu_baseline"]["value"] and fin["cpu_baseline"]["cores"] == 2
+    # the sweep ends one point past the job's vector, as the reference's campaign (2^27 ints)
+    sweep = fin["size_sweep_us"]
+    assert sweep[str(8 * 65536)]["raben_us"] > 0 and sweep[str(8 * 65536)]["rd_us"] > 0, sweep
     assert took < 150, took
 
 

@@ -212,7 +212,10 @@ def test_random_external_kill_never_wrong(hostsim, oracle, seed):
     kids = [c for c in _children(p.pid) if "main" in c[2]]
     if kids:
         victim = int(rng.choice(kids)[0])
-        os.kill(victim, signal.SIGKILL)
+        try:
+            os.kill(victim, signal.SIGKILL)
+        except ProcessLookupError:
+            pass  # the rank had already finished: a no-fault run, checked the same way
     out, err = p.communicate(timeout=120)
     hello = {int(l.split()[2]): int(l.split()[-1]) for l in out.splitlines() if l.startswith("Hello")}
     aborted = any(l.split() and l.split()[0] == "MPI_ABORT" for l in err.splitlines())
