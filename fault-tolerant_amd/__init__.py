@@ -28,6 +28,7 @@ PT_BEFORE, PT_AFTER, PT_BARRIER, PT_DURING = 0, 1, 2, 3
 OPT_OVERLAP, OPT_RELAY, OPT_RELAY_MIN, OPT_LOOP_SECONDS, OPT_COPY_ENGINE, OPT_REDUNDANCY, OPT_MESH = 0, 1, 2, 3, 4, 5, 6
 OPT_ONESHOT_MAX = 7
 OPT_PUSH = 8
+OPT_GATE = 9
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
 ERR_OP = 9  # MPI_ERR_OP: a logical / bitwise op on a float type
 
@@ -43,7 +44,8 @@ class Stats(ctypes.Structure):
                 ("hbm_bytes", ctypes.c_double), ("kernels", ctypes.c_int), ("step0_link_bytes", ctypes.c_double),
                 ("bg_kernel_ms", ctypes.c_double), ("sync_wait_s", ctypes.c_double),
                 ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int), ("relayed_steps", ctypes.c_int),
-                ("mesh_steps", ctypes.c_int), ("export_retries", ctypes.c_int)]
+                ("mesh_steps", ctypes.c_int), ("export_retries", ctypes.c_int),
+                ("gated_launches", ctypes.c_int), ("gated_skips", ctypes.c_int)]
 
 
 class Kill(ctypes.Structure):

@@ -158,6 +158,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
     c->push = getenv("FTAR_PUSH") ? atoi(getenv("FTAR_PUSH")) : 0;
+    c->gate = getenv("FTAR_GATE") ? atoi(getenv("FTAR_GATE")) != 0 : 1;
     c->oneshot_max = getenv("FTAR_ONESHOT_MAX") ? (size_t)atoll(getenv("FTAR_ONESHOT_MAX")) : ((size_t)1 << 20);
     c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
     c->stage_max = getenv("FTAR_STAGE_MAX") ? (size_t)atoll(getenv("FTAR_STAGE_MAX")) : ((size_t)1 << 20);
@@ -435,6 +436,7 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_MESH: c->mesh = v != 0; break;
     case FTAR_OPT_ONESHOT_MAX: c->oneshot_max = (size_t)v; break;
     case FTAR_OPT_PUSH: c->push = v >= 2 ? 2 : v != 0; break;
+    case FTAR_OPT_GATE: c->gate = v != 0; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;
@@ -453,6 +455,7 @@ int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
     case FTAR_OPT_MESH: *v = c->mesh; break;
     case FTAR_OPT_ONESHOT_MAX: *v = (double)c->oneshot_max; break;
     case FTAR_OPT_PUSH: *v = c->push; break;
+    case FTAR_OPT_GATE: *v = c->gate; break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;

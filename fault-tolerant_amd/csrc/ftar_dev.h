@@ -104,6 +104,21 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
 #define FDEV_MAX_BATCH 8
 int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
                     void *const *out, const size_t *n, int ntree, int tag);
+/* The same batch queued AHEAD of the barrier that makes its operands ready: the launch's
+ * workgroups wait on a gate word in pinned host memory until fdev_gate_open (go: they
+ * run; skip: they return without touching memory), so the launch latency overlaps the
+ * wait for the peers.  Only a short signalled launch can be gated, and only when every
+ * launch queued since the last drain signalled (a fenced marker would wait behind the
+ * closed gate): *gated = 0 and nothing is queued otherwise (and with kernel timing on).
+ * Until the gate opens, fdev_sync waits for the launches queued BEFORE it only; nothing
+ * may be queued behind a closed gate. */
+int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
+                          const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
+                          int *gated);
+/* Open the pending gate (no-op without one).  skip = 1: the gated launch does nothing. */
+int fdev_gate_open(ftar_dev *d, int skip);
+/* 1 while a gated launch waits for its gate. */
+int fdev_gate_pending(const ftar_dev *d);
 /* Enqueue on the rank's background stream, ordered after everything queued so far on
  * the main stream (it then overlaps later main-stream work). */
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);

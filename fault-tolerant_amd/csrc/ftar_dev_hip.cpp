@@ -130,6 +130,17 @@ struct ftar_dev {
     int need_acquire;      // the last drain was a signal: no marker has invalidated the caches since
     int force_fence;       // the next drain must be a fenced marker (peers read caller memory in place)
     int waited_user;       // a wait on the caller's stream was queued since the last drain
+    // A launch queued ahead of its barrier (fdev_tree_batch_gated): its workgroups wait on
+    // the gate word (sig_flag[16]) until fdev_gate_open; a timed-out gate is reported in
+    // sig_flag[32].
+    unsigned gate_seq;     // sequence of the last gate (the word's value = 2 x seq, + 1 = skip)
+    int gate_pending;      // queued, gate still closed
+    int gate_verify;       // opened: check the timeout word at the next drain
+    int after_gate;        // something was queued behind the closed gate (a misuse: refused at the drain)
+    int pre_gate_any;      // signalled launches queued before the gated one since the last drain ...
+    unsigned pre_gate_tag; // ... the last of them
+    unsigned long long gate_ticks; // wall-clock ticks before a closed gate counts as timed out
+    double gate_link, gate_hbm;    // the gated launch's bytes (counted if it runs)
 };
 
 extern "C" {
@@ -176,6 +187,15 @@ int fdev_open(int device, ftar_dev **out)
         d->sig_flag = nullptr;
         d->sig_tag = 0;
         d->unsignalled = d->signalled = d->need_acquire = d->force_fence = d->waited_user = 0;
+        d->gate_seq = 0;
+        d->gate_pending = d->gate_verify = d->after_gate = d->pre_gate_any = 0;
+        d->pre_gate_tag = 0;
+        int khz = 0; // wall clock of the kernels (s_memrealtime), 100 MHz on CDNA
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
+            (void)hipGetLastError();
+            khz = 100000;
+        }
+        d->gate_ticks = (unsigned long long)khz * 1000ull * 60ull; // 60 s
         if (d->flag_sync) {
             HIPCHK(hipMalloc((void **)&d->sig_cnt, 256));
             HIPCHK(hipMemset(d->sig_cnt, 0, 256));
@@ -189,6 +209,7 @@ int fdev_open(int device, ftar_dev **out)
                 d->sig_cnt = nullptr;
                 d->flag_sync = 0;
             } else {
+                memset(d->sig_flag, 0, 256); // flag [0], gate [16], gate timeout [32]
                 __atomic_store_n(d->sig_flag, 0u, __ATOMIC_RELEASE);
             }
             HIPCHK(hipDeviceSynchronize());
@@ -214,6 +235,7 @@ void fdev_close(ftar_dev *d)
 {
     if (!d) return;
     (void)hipSetDevice(d->device);
+    (void)fdev_gate_open(d, 1); // a launch still waiting on its gate returns without work
     (void)hipStreamSynchronize(d->stream);
     if (d->bg) (void)hipStreamSynchronize(d->bg);
     if (d->h2d) (void)hipStreamSynchronize(d->h2d);
@@ -418,6 +440,7 @@ static hipEvent_t get_event(ftar_dev *d)
 static void note_launch(ftar_dev *d, hipStream_t st, unsigned grid, bool can_signal, ftar::KSignal *sig)
 {
     if (sig) *sig = ftar::KSignal{nullptr, nullptr, 0, 0};
+    if (d->gate_pending) d->after_gate = 1; // queued behind a closed gate (both streams wait on it)
     if (st != d->stream) {
         if (d->need_acquire && d->fence_bg) (void)hipEventRecord(d->fence_bg, st);
         return;
@@ -527,8 +550,11 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
     return 0;
 }
 
-int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
-                    void *const *out, const size_t *n, int ntree, int tag)
+// The TreeBatch of fdev_tree_batch(_gated): the grid (0 = a tree beyond the workgroup
+// budget, or nothing to do when B->nt == 0), link and HBM bytes.
+static int build_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
+                       void *const *out, const size_t *n, int ntree, int tag, ftar::TreeBatch *B, unsigned *grid,
+                       double *link, double *hbm)
 {
     size_t es = esize_of(dtype);
     if (es == 0 || op < 0 || op >= ftar::kNumOps || tag < 0 || tag >= FDEV_NTAGS || ntree < 1 || ntree > ftar::kMaxBatch ||
@@ -536,23 +562,76 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
         snprintf(g_err, sizeof(g_err), "fdev_tree_batch: bad arguments");
         return 13;
     }
-    ftar::TreeBatch B;
-    memset(&B, 0, sizeof(B));
-    B.nt = 0;
-    double link = 0, hbm = 0;
+    memset(B, 0, sizeof(*B));
+    B->nt = 0;
+    *link = *hbm = 0;
     for (int t = 0; t < ntree; t++) {
         if (n[t] == 0) continue;
-        ftar::TreeArgs &A = B.t[B.nt++];
+        ftar::TreeArgs &A = B->t[B->nt++];
         for (int j = 0; j < nsrc; j++) A.src[j] = src[t * nsrc + j];
         A.out = out[t];
         A.n = n[t];
         A.nt_store = nt_store();
         int nremote = __builtin_popcount(remote_mask[t] & ((1u << nsrc) - 1));
-        link += (double)n[t] * (double)es * nremote;
-        hbm += (double)n[t] * (double)es * (nsrc - nremote + 1);
+        *link += (double)n[t] * (double)es * nremote;
+        *hbm += (double)n[t] * (double)es * (nsrc - nremote + 1);
     }
-    if (B.nt == 0) return 0;
-    unsigned grid = ftar::plan_tree_batch(&B, nsrc, es, d->max_blocks + 1);
+    *grid = B->nt ? ftar::plan_tree_batch(B, nsrc, es, d->max_blocks + 1) : 0;
+    return 0;
+}
+
+int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
+                          const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag, int *gated)
+{
+    *gated = 0;
+    // a fenced marker or an unsignalled launch would have to drain behind the closed gate
+    if (!d->flag_sync || d->profiling || d->gate_pending || d->unsignalled || d->force_fence) return 0;
+    ftar::TreeBatch B;
+    unsigned grid = 0;
+    double link, hbm;
+    int rc = build_batch(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, &B, &grid, &link, &hbm);
+    if (rc || grid == 0 || grid > d->flag_max) return rc;
+    d->gate_link = link; // counted when the gate opens to run it
+    d->gate_hbm = hbm;
+    d->pre_gate_any = d->signalled > 0;
+    d->pre_gate_tag = d->sig_tag;
+    d->gate_seq++;
+    // the workgroups invalidate their caches once the gate opens (acquire = 1): whatever
+    // the drains before it did, the peers' data is read fresh
+    B.sig = ftar::KSignal{d->sig_cnt, d->sig_flag, ++d->sig_tag, 1u, d->sig_flag + 16, 2u * d->gate_seq,
+                          d->sig_flag + 32, d->gate_ticks};
+    d->signalled++;
+    hipError_t e = ftar::launch_tree_batch(dtype, op, nsrc, B, grid, d->stream);
+    if (e != hipSuccess) return set_err(e, "tree_batch_kernel launch (gated)");
+    d->gate_pending = 1;
+    d->after_gate = 0;
+    *gated = 1;
+    return 0;
+}
+
+int fdev_gate_open(ftar_dev *d, int skip)
+{
+    if (!d->gate_pending) return 0;
+    __atomic_store_n(d->sig_flag + 16, 2u * d->gate_seq + (skip ? 1u : 0u), __ATOMIC_RELEASE);
+    if (!skip) {
+        d->ctr.link_bytes += d->gate_link;
+        d->ctr.hbm_bytes += d->gate_hbm;
+    }
+    d->gate_pending = 0;
+    d->gate_verify = 1;
+    return 0;
+}
+
+int fdev_gate_pending(const ftar_dev *d) { return d->gate_pending; }
+
+int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
+                    void *const *out, const size_t *n, int ntree, int tag)
+{
+    ftar::TreeBatch B;
+    unsigned grid = 0;
+    double link, hbm;
+    int rc = build_batch(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, &B, &grid, &link, &hbm);
+    if (rc || B.nt == 0) return rc;
     if (grid == 0) { // a tree beyond the workgroup budget: one (split) launch per tree
         for (int t = 0; t < ntree; t++) {
             int rc = fdev_tree(d, dtype, op, src + (size_t)t * nsrc, nsrc, remote_mask[t], out[t], n[t], tag);
@@ -697,6 +776,21 @@ static int wait_signal(ftar_dev *d, unsigned tag, int (*poll)(void *), void *arg
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 {
     int rc;
+    if (d->gate_pending) {
+        // a launch waits on its closed gate: drain what was queued before it (all of it
+        // signalled, fdev_tree_batch_gated checked), never a marker behind the gate
+        if (d->after_gate) {
+            snprintf(g_err, sizeof(g_err), "fdev_sync: work queued behind a closed gate");
+            return 13;
+        }
+        rc = d->pre_gate_any ? wait_signal(d, d->pre_gate_tag, poll, arg) : 0;
+        d->need_acquire = 1;
+        d->pre_gate_any = 0;
+        d->unsignalled = d->waited_user = d->force_fence = 0;
+        d->signalled = 1; // the gated launch, drained after its gate opens
+        if (rc) return rc;
+        return harvest(d);
+    }
     if (!d->unsignalled && !d->signalled && !d->waited_user && !d->force_fence) {
         rc = 0; // nothing queued since the last drain
     } else if (!d->unsignalled && d->signalled && !d->force_fence) {
@@ -710,6 +804,15 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
     }
     d->unsignalled = d->signalled = d->waited_user = d->force_fence = 0;
     if (rc) return rc;
+    if (d->gate_verify) { // the gated launch has completed: did its gate time out?
+        d->gate_verify = 0;
+        unsigned t = __atomic_load_n(d->sig_flag + 32, __ATOMIC_ACQUIRE);
+        if (t) {
+            __atomic_store_n(d->sig_flag + 32, 0u, __ATOMIC_RELAXED);
+            snprintf(g_err, sizeof(g_err), "gated launch %u: its gate stayed closed past the timeout", t / 2);
+            return 101;
+        }
+    }
     return harvest(d);
 }
 

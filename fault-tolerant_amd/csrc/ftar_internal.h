@@ -85,6 +85,7 @@ struct ftar_comm {
     int redundancy;      /* FTAR_REDUNDANCY (default 0: the step-0 copy is never moved; a replay reads the dead rank's IN) */
     int mesh;            /* FTAR_MESH (default 1): one-hop Raben at power-of-two p without a spare */
     int push;            /* FTAR_PUSH (default 0): the mesh by remote stores -- 1 reduce-scatter, 2 both phases */
+    int gate;            /* FTAR_GATE (default 1): small one-shot launch queued ahead of its barrier, gated */
     size_t oneshot_max;  /* FTAR_ONESHOT_MAX bytes: mesh Raben in one launch up to this size */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
     /* the step's last peer read (FTAR_LOOP_SECONDS re-pulls it into pad while it waits) */

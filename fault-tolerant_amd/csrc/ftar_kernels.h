@@ -25,11 +25,22 @@ constexpr int kMaxIleave = 16; // vector pieces that can share the interleaved p
 // cached copies of remote memory (system-scope acquire) -- the host sets it when the last
 // drain was such a signal, i.e. no marker packet has invalidated the caches since the
 // barrier after which this launch reads the peers' new data.
+//
+// `gate` (optional): the launch was queued before the host barrier that makes its
+// operands ready.  Thread 0 of every workgroup polls the pinned host word (system scope)
+// until it reaches gate_val (= 2 x sequence, bit 0 set = skip), the workgroup then runs or
+// returns without touching memory; either way it signals.  A gate still closed after
+// gate_ticks of the wall clock (tens of seconds: the host never got past its barrier) is
+// taken as skip and reported through `err`, which the host checks after the drain.
 struct KSignal {
     unsigned *cnt;  // device counter, agent-scope atomics; nullptr = no signal
     unsigned *flag; // pinned host word
     unsigned tag;
     unsigned acquire;
+    const unsigned *gate; // pinned host word; nullptr = not gated
+    unsigned gate_val;
+    unsigned *err;        // pinned host word: set to gate_val on a gate timeout
+    unsigned long long gate_ticks;
 };
 
 struct KSeg {

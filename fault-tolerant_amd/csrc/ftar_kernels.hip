@@ -142,6 +142,34 @@ __device__ __forceinline__ void signal_acquire(const KSignal &G)
     }
 }
 
+// The gate of a launch queued ahead of its barrier (KSignal): 1 = run, 0 = skip.  One
+// lane polls the host word with system-scope loads (uncached, over PCIe), sleeping
+// between polls; the workgroup learns the verdict through LDS.  Uniform over the launch.
+__device__ __forceinline__ bool signal_gate(const KSignal &G)
+{
+    if (!G.gate) return true;
+    __shared__ unsigned go;
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = wall_clock64();
+        unsigned v;
+        for (;;) {
+            v = __hip_atomic_load(G.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((int)((v & ~1u) - (G.gate_val & ~1u)) >= 0) break;
+            if (wall_clock64() - t0 > G.gate_ticks) { // the host never opened it: skip, report
+                __hip_atomic_store(G.err, G.gate_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                v = G.gate_val | 1u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        // one gate at a time: the host arms the next only after this launch has drained,
+        // so the word holds our sequence, and its bit 0 is the verdict
+        go = (v == G.gate_val) ? 1u : 0u;
+    }
+    __syncthreads();
+    return go != 0;
+}
+
 __device__ __forceinline__ void signal_done(const KSignal &G)
 {
     if (!G.cnt) return;
@@ -317,8 +345,10 @@ __global__ __launch_bounds__(kBlock) void tree_batch_kernel(TreeBatch B)
     const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     int k = 0;
     while (k + 1 < B.nt && b >= B.first[k + 1]) k++;
-    signal_acquire(B.sig);
-    tree_body<T, OP, P>(B.t[k], b - B.first[k], B.first[k + 1] - B.first[k]);
+    if (signal_gate(B.sig)) {
+        signal_acquire(B.sig);
+        tree_body<T, OP, P>(B.t[k], b - B.first[k], B.first[k + 1] - B.first[k]);
+    }
     signal_done(B.sig);
 }
 

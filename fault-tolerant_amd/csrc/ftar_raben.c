@@ -52,6 +52,15 @@ typedef struct {
     int push;       /* the mesh's reduce-scatter by remote stores into the owners' R (FTAR_OPT_PUSH) */
     int64_t slot;   /* push: elements per source slot in an owner's R */
     int oneshot;    /* mesh of a small vector: every block in its owner's tree, one launch */
+    /* the one-shot launch queued ahead of the barrier (rb_oneshot_prelaunch): its plan, to
+     * be checked against the one the inputs' resolution gives */
+    int gated;
+    struct rb_batch {
+        const void *src[FDEV_MAX_BATCH * FDEV_MAX_BATCH];
+        void *out[FDEV_MAX_BATCH];
+        size_t n[FDEV_MAX_BATCH];
+        unsigned remote[FDEV_MAX_BATCH];
+    } gplan;
     int in0_w[FTAR_MAX_RANKS]; /* world rank whose IN held vrank v's input at RS step 0 */
     int64_t rindex[MAXSTEPS], sindex[MAXSTEPS], rcount[MAXSTEPS], scount[MAXSTEPS];
 } rb_ctx;
@@ -511,40 +520,73 @@ allgather:
  * per rank instead of 2 (p-1) S / p -- cheaper below the size where a launch + drain
  * (~11 us) outweighs the extra link time.  Kill points and the two agree rounds are
  * rb_mesh's; with no idle rank a failure anywhere aborts. */
-static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
+/* The one-shot launch's operands as the peers' inputs stand now (ftar_buf: a peer's
+ * exported sbuf once ftar_resolve_inputs mapped it, else its staged IN). */
+static void rb_oneshot_plan(rb_ctx *x, const void *sbuf, void *rbuf, struct rb_batch *B)
 {
     ftar_comm *c = x->c;
     const int L = x->steps, p = x->adjsize, v = x->vrank;
-    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BEFORE);
-    ftar_enter(c);
-    const void *src[FDEV_MAX_BATCH * FDEV_MAX_BATCH];
-    void *out[FDEV_MAX_BATCH];
-    size_t n[FDEV_MAX_BATCH];
-    unsigned remote[FDEV_MAX_BATCH];
+    memset(B, 0, sizeof(*B));
     for (int u = 0; u < p; u++) { /* block owned by vrank u */
         int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
         rb_windows(u, x->count, L, ri, si, rc, sc);
         const int64_t off = ri[L - 1];
-        out[u] = at(x, rbuf, off);
-        n[u] = (size_t)rc[L - 1];
-        remote[u] = 0;
+        B->out[u] = at(x, rbuf, off);
+        B->n[u] = (size_t)rc[L - 1];
         for (int j = 0; j < p; j++) {
             const int w = u ^ j;
             if (w == v) {
-                src[u * p + j] = at(x, (void *)sbuf, off);
+                B->src[u * p + j] = at(x, (void *)sbuf, off);
             } else {
-                src[u * p + j] = at(x, ftar_buf(c, c->order[rb_real(x, w)], WS_IN), off);
-                remote[u] |= 1u << j;
+                B->src[u * p + j] = at(x, ftar_buf(c, c->order[rb_real(x, w)], WS_IN), off);
+                B->remote[u] |= 1u << j;
             }
         }
     }
+}
+
+/* Queue the one-shot launch right behind this rank's staging copy, before the barrier
+ * after which the peers' staged inputs may be read: its workgroups wait on a gate that
+ * rb_oneshot opens at the point where it would otherwise launch, so the launch latency
+ * overlaps the staging drain and the barrier.  The plan assumes every peer stages its
+ * input (this rank did, so the size is the same everywhere); rb_oneshot re-plans after
+ * the inputs are resolved and skips the gated launch if anything differs. */
+static void rb_oneshot_prelaunch(rb_ctx *x, const void *sbuf, void *rbuf)
+{
+    ftar_comm *c = x->c;
+    x->gated = 0;
+    if (!c->gate) return;
+    rb_oneshot_plan(x, sbuf, rbuf, &x->gplan);
+    if (fdev_tree_batch_gated(c->dev, x->dtype, x->op, x->gplan.src, x->adjsize, x->gplan.remote, x->gplan.out,
+                              x->gplan.n, x->adjsize, FDEV_TAG_STEP0, &x->gated)) {
+        fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    if (x->gated) c->stats.gated_launches++;
+}
+
+static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
+{
+    ftar_comm *c = x->c;
+    const int L = x->steps, p = x->adjsize;
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BEFORE);
+    ftar_enter(c);
+    struct rb_batch B;
+    rb_oneshot_plan(x, sbuf, rbuf, &B);
+    const void *const *src = B.src;
     double lb0 = ftar_link_bytes(c);
     for (int k = 0; k < p * p; k++) /* the first peer operand: the padding's re-pull source */
-        if (remote[k / p] & (1u << (k % p))) {
-            ftar_note_launch(c, src[k], n[k / p] * x->es);
+        if (B.remote[k / p] & (1u << (k % p))) {
+            ftar_note_launch(c, src[k], B.n[k / p] * x->es);
             break;
         }
-    if (fdev_tree_batch(c->dev, x->dtype, x->op, src, p, remote, out, n, p, FDEV_TAG_STEP0)) {
+    int go = x->gated && memcmp(&B, &x->gplan, sizeof(B)) == 0;
+    if (x->gated) { /* the queued launch runs now, or returns untouched and is replaced */
+        fdev_gate_open(c->dev, !go);
+        if (!go) c->stats.gated_skips++;
+        x->gated = 0;
+    }
+    if (!go && fdev_tree_batch(c->dev, x->dtype, x->op, src, p, B.remote, B.out, B.n, p, FDEV_TAG_STEP0)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
@@ -666,6 +708,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     } else if (x->oneshot) {
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         run_copy(x, IN, sbuf, (int64_t)count, 0, FDEV_TAG_LOCAL);
+        /* small inputs are staged by every rank (ftar_stage_input): the launch's operands
+         * are known before the barrier */
+        if (bytes <= c->stage_max) rb_oneshot_prelaunch(x, sbuf, rbuf);
     } else if (x->mesh) { /* peers pull every block of sbuf but this rank's own final one */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         int64_t b0 = x->rindex[x->steps - 1], b1 = b0 + x->rcount[x->steps - 1];

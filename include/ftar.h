@@ -199,10 +199,13 @@ typedef enum {
                                   allgather over the full mesh, same reduction tree (0/1) */
     FTAR_OPT_ONESHOT_MAX = 7,  /* mesh Raben up to this many bytes per vector (any size at p = 2): one
                                   launch computes every block in its owner's tree into rbuf (0 = off) */
-    FTAR_OPT_PUSH = 8          /* mesh Raben by remote stores: 1 = reduce-scatter (every rank writes its part
+    FTAR_OPT_PUSH = 8,         /* mesh Raben by remote stores: 1 = reduce-scatter (every rank writes its part
                                   of each block into the owner's HBM, the owner reduces locally), 2 = both
                                   phases (the owner's tree also stores its block into every peer; p <= 8),
                                   0 = remote loads (default) */
+    FTAR_OPT_GATE = 9          /* queue the small one-shot launch ahead of the barrier that readies its
+                                  operands, its workgroups waiting on a gate the barrier opens (0/1,
+                                  default 1): the launch latency overlaps the wait for the peers */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);
@@ -228,6 +231,8 @@ typedef struct {
     int    mesh_steps;       /* one-hop mesh exchanges (Raben reduce-scatter / allgather) */
     int    export_retries;   /* workspace blocks the runtime refused to export (IPC) and that were
                                 re-allocated, cumulative since ftar_init (expected: 0) */
+    int    gated_launches;   /* launches queued ahead of their barrier (FTAR_OPT_GATE) */
+    int    gated_skips;      /* ... of them replaced after the barrier (a peer's input moved) */
 } ftar_stats;
 
 int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);

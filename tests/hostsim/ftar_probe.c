@@ -60,6 +60,16 @@ int main(void)
     int inplace = getenv("FTAR_PROBE_INPLACE") ? atoi(getenv("FTAR_PROBE_INPLACE")) : 0;
     size_t off = getenv("FTAR_PROBE_OFFSET") ? strtoull(getenv("FTAR_PROBE_OFFSET"), NULL, 10) : 0;
 
+    /* FTAR_PROBE_RANK_ENV="r:NAME=VALUE": one rank's own setting (a knob the launcher would
+     * otherwise give every rank alike) */
+    const char *re = getenv("FTAR_PROBE_RANK_ENV"), *me = getenv("FTAR_RANK");
+    if (re && me && atoi(re) == atoi(me) && strchr(re, ':') && strchr(re, '=')) {
+        char kv[256];
+        snprintf(kv, sizeof(kv), "%s", strchr(re, ':') + 1);
+        char *eq = strchr(kv, '=');
+        *eq = 0;
+        setenv(kv, eq + 1, 1);
+    }
     ftar_comm *comm;
     if (ftar_init(&comm) != FTAR_SUCCESS) return 3;
     int rank;
@@ -104,9 +114,9 @@ int main(void)
         fclose(f);
         snprintf(path, sizeof(path), "%s/status_%d_%d.txt", dir, rank, it);
         f = fopen(path, "w");
-        fprintf(f, "%d %d %d %d %lld %lld %lld %d %d %d\n", rc, crank, csize, st.recoveries,
+        fprintf(f, "%d %d %d %d %lld %lld %lld %d %d %d %d %d\n", rc, crank, csize, st.recoveries,
                 (long long)(st.wall_s * 1e6), (long long)(st.sync_wait_s * 1e6), (long long)(st.drain_s * 1e6), st.syncs,
-                st.relayed_steps, st.mesh_steps);
+                st.relayed_steps, st.mesh_steps, st.gated_launches, st.gated_skips);
         fclose(f);
     }
     ftar_finalize(comm);

@@ -16,6 +16,7 @@
 #   campaign   tools/fault_campaign.sh: the reference's random-kill campaign, both schedules
 #   sweep      tools/size_sweep.py with 2 / 4 / 8 ranks on GPU 0
 #   e2e        host-buffer Raben end to end: chunk pipeline on / off, zero copy (1 / 2 / 4 ranks)
+#   latency    tools/latency_probe.py with 2 / 4 / 8 ranks on GPU 0 (gated one-shot vs not)
 #   syncprobe  tools/sync_probe.hip: device round trip of one step
 #   cpubase    tools/cpu_schedule_bench.py on this box's host cores
 #   xgmi       tools/xgmi_probe.hip: one link / all peers, pull / push / copy engines (loopback on one GPU)
@@ -111,6 +112,16 @@ if has e2e; then
     rc=$?; stop_on_fault $rc e2e_${n}_$mode
   done; done
   cat "$OUT/e2e.json"
+fi
+if has latency; then
+  # per-call fixed cost of a 4 KiB call, ranks sharing GPU 0 (tools/latency_probe.py):
+  # one-shot with its launch gated ahead of the barrier vs launched after it, mesh, RD
+  for n in ${LAT_RANKS:-2 4 8}; do
+    DM=$(python3 -c "print(','.join(['0']*$n))")
+    timeout -k 10 180 fault-tolerant_amd/bin/ftrun -np $n --devmap $DM python -u tools/latency_probe.py \
+        "$OUT/latency_${n}ranks.json" > "$OUT/latency_${n}ranks.log" 2>&1
+    rc=$?; tail -c 400 "$OUT/latency_${n}ranks.log"; echo; stop_on_fault $rc latency_$n
+  done
 fi
 if has syncprobe; then
   timeout -k 10 120 tools/_build/sync_probe > "$OUT/sync_probe.json" 2>&1

@@ -49,12 +49,17 @@ def main():
     res["ftar_barrier_us"] = med(ts)
     for prof in (0, 1):
         comm.set_profiling(bool(prof))
-        for name, fn, limit in (("raben_oneshot", comm.allreduce_rabenseifner, 1 << 20),
-                                ("raben_mesh", comm.allreduce_rabenseifner, 0), ("rd", comm.recursive_doubling, 0)):
+        # raben_oneshot: its launch queued ahead of the barrier behind a gate (FTAR_OPT_GATE,
+        # the default); raben_oneshot_nogate: launched after the barrier (round 3's first form)
+        for name, fn, limit, gate in (("raben_oneshot", comm.allreduce_rabenseifner, 1 << 20, 1),
+                                      ("raben_oneshot_nogate", comm.allreduce_rabenseifner, 1 << 20, 0),
+                                      ("raben_mesh", comm.allreduce_rabenseifner, 0, 1),
+                                      ("rd", comm.recursive_doubling, 0, 1)):
             comm.set_option(ftar.OPT_ONESHOT_MAX, limit)
+            comm.set_option(ftar.OPT_GATE, gate)
             for _ in range(5):
                 assert fn(x, y) == 0
-            wall, drain, sync, kern, cwall = [], [], [], [], []
+            wall, drain, sync, kern, cwall, gated = [], [], [], [], [], []
             for _ in range(200):
                 comm.barrier()
                 t0 = time.perf_counter()
@@ -65,14 +70,16 @@ def main():
                 sync.append(st.sync_wait_s)
                 kern.append(st.step0_kernel_ms * 1e-3)
                 cwall.append(st.wall_s)
+                gated.append(st.gated_launches)
             key = name + ("_profiled" if prof else "")
             # wall: the Python call; c_wall: inside the C entry point (ftar_stats wall_s,
             # what a C caller of include/ftar.h pays, minus the argument checks)
             res[key] = {"wall_us": med(wall), "c_wall_us": med(cwall), "drain_us": med(drain),
-                        "sync_wait_us": med(sync)}
+                        "sync_wait_us": med(sync), "gated_calls": sum(1 for g in gated if g)}
             if prof:
                 res[key]["step0_kernel_us"] = med(kern)
     comm.set_option(ftar.OPT_ONESHOT_MAX, 1 << 20)
+    comm.set_option(ftar.OPT_GATE, 1)
     if rank == 0:
         print(json.dumps(res), flush=True)
         if len(sys.argv) > 1:
