@@ -578,6 +578,44 @@ static void note_segs(ftar_comm *c, int dtype, const fdev_seg *segs, int nseg)
         atomic_store_explicit(&c->job.shm->slot[c->wrank].inflight, FTAR_INFLIGHT_PULL, memory_order_release);
 }
 
+int ftar_prelaunch(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    int gated = 0;
+    c->gplan.valid = 0;
+    if (!c->gate || nseg <= 0 || nseg > FDEV_MAX_SEGS) return 0;
+    if (fdev_run_gated(c->dev, dtype, op, segs, nseg, tag, &gated)) {
+        fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    if (!gated) return 0;
+    c->gplan = (struct ftar_gplan){1, dtype, op, tag, nseg, {{0}}};
+    memcpy(c->gplan.segs, segs, sizeof(fdev_seg) * (size_t)nseg);
+    c->stats.gated_launches++;
+    return 1;
+}
+
+static int seg_eq(const fdev_seg *a, const fdev_seg *b)
+{
+    return a->kind == b->kind && a->remote == b->remote && a->out == b->out && a->x == b->x &&
+           (a->kind == FDEV_COPY || a->y == b->y) && a->n == b->n && a->out2 == b->out2;
+}
+
+void ftar_run_gated_or(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+{
+    int pending = fdev_gate_pending(c->dev);
+    int go = pending && c->gplan.valid && c->gplan.dtype == dtype && c->gplan.op == op && c->gplan.tag == tag &&
+             c->gplan.nseg == nseg;
+    for (int i = 0; go && i < nseg; i++) go = seg_eq(&segs[i], &c->gplan.segs[i]);
+    if (c->gplan.valid && !go) c->stats.gated_skips++; /* given up here, or already by another launch */
+    c->gplan.valid = 0;
+    if (pending) fdev_gate_open(c->dev, !go);
+    if (go) {
+        note_segs(c, dtype, segs, nseg);
+        return;
+    }
+    if (nseg) ftar_run(c, dtype, op, segs, nseg, tag);
+}
+
 int ftar_drain(ftar_comm *c)
 {
     double t0 = now_s();

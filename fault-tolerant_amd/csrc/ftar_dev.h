@@ -110,12 +110,16 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
  * wait for the peers.  Only a short signalled launch can be gated, and only when every
  * launch queued since the last drain signalled (a fenced marker would wait behind the
  * closed gate): *gated = 0 and nothing is queued otherwise (and with kernel timing on).
- * Until the gate opens, fdev_sync waits for the launches queued BEFORE it only; nothing
- * may be queued behind a closed gate. */
+ * Until the gate opens, fdev_sync waits for the launches queued BEFORE it only. */
 int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
                           const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
                           int *gated);
-/* Open the pending gate (no-op without one).  skip = 1: the gated launch does nothing. */
+/* fdev_run's segment kernel queued behind a gate, on the same terms. */
+int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int *gated);
+/* Open the pending gate (no-op without one).  skip = 1: the gated launch does nothing.
+ * Any other launch or stream wait queued while a gate is pending opens it as skip first
+ * (nothing may wait behind a closed gate): a caller about to open its gate checks
+ * fdev_gate_pending and relaunches if the gated launch was given up. */
 int fdev_gate_open(ftar_dev *d, int skip);
 /* 1 while a gated launch waits for its gate. */
 int fdev_gate_pending(const ftar_dev *d);

@@ -130,13 +130,12 @@ struct ftar_dev {
     int need_acquire;      // the last drain was a signal: no marker has invalidated the caches since
     int force_fence;       // the next drain must be a fenced marker (peers read caller memory in place)
     int waited_user;       // a wait on the caller's stream was queued since the last drain
-    // A launch queued ahead of its barrier (fdev_tree_batch_gated): its workgroups wait on
-    // the gate word (sig_flag[16]) until fdev_gate_open; a timed-out gate is reported in
-    // sig_flag[32].
+    // A launch queued ahead of its barrier (fdev_tree_batch_gated / fdev_run_gated): its
+    // workgroups wait on a gate word (sig_flag[16 + seq % 8]) until fdev_gate_open; a gate
+    // that timed out (or was found overtaken) is reported in sig_flag[32].
     unsigned gate_seq;     // sequence of the last gate (the word's value = 2 x seq, + 1 = skip)
     int gate_pending;      // queued, gate still closed
     int gate_verify;       // opened: check the timeout word at the next drain
-    int after_gate;        // something was queued behind the closed gate (a misuse: refused at the drain)
     int pre_gate_any;      // signalled launches queued before the gated one since the last drain ...
     unsigned pre_gate_tag; // ... the last of them
     unsigned long long gate_ticks; // wall-clock ticks before a closed gate counts as timed out
@@ -188,7 +187,7 @@ int fdev_open(int device, ftar_dev **out)
         d->sig_tag = 0;
         d->unsignalled = d->signalled = d->need_acquire = d->force_fence = d->waited_user = 0;
         d->gate_seq = 0;
-        d->gate_pending = d->gate_verify = d->after_gate = d->pre_gate_any = 0;
+        d->gate_pending = d->gate_verify = d->pre_gate_any = 0;
         d->pre_gate_tag = 0;
         int khz = 0; // wall clock of the kernels (s_memrealtime), 100 MHz on CDNA
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
@@ -440,7 +439,9 @@ static hipEvent_t get_event(ftar_dev *d)
 static void note_launch(ftar_dev *d, hipStream_t st, unsigned grid, bool can_signal, ftar::KSignal *sig)
 {
     if (sig) *sig = ftar::KSignal{nullptr, nullptr, 0, 0};
-    if (d->gate_pending) d->after_gate = 1; // queued behind a closed gate (both streams wait on it)
+    // anything queued behind a closed gate would wait for it: the gated launch is given up
+    // (opened as skip; it returns untouched) -- its caller finds the gate no longer pending
+    if (d->gate_pending) (void)fdev_gate_open(d, 1);
     if (st != d->stream) {
         if (d->need_acquire && d->fence_bg) (void)hipEventRecord(d->fence_bg, st);
         return;
@@ -550,6 +551,33 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
     return 0;
 }
 
+// Gate words: sig_flag[16 .. 23], gate `seq` in slot seq % kGateSlots.
+static unsigned *gate_word(ftar_dev *d, unsigned seq) { return d->sig_flag + 16 + seq % ftar::kGateSlots; }
+
+// Whether a launch of `grid` workgroups may be queued behind a gate now (see
+// fdev_tree_batch_gated): a fenced marker or an unsignalled launch would have to drain
+// behind the closed gate, a profiled launch would time the wait.
+static bool can_gate(const ftar_dev *d, unsigned grid)
+{
+    return d->flag_sync && !d->profiling && !d->gate_pending && !d->unsignalled && !d->force_fence && grid > 0 &&
+           grid <= d->flag_max;
+}
+
+// The gate fields of a launch about to be queued gated; its bytes are counted when it runs.
+static ftar::KSignal arm_gate(ftar_dev *d, double link, double hbm)
+{
+    d->gate_link = link;
+    d->gate_hbm = hbm;
+    d->pre_gate_any = d->signalled > 0;
+    d->pre_gate_tag = d->sig_tag;
+    d->gate_seq++;
+    d->signalled++;
+    // the workgroups invalidate their caches once the gate opens (acquire = 1): whatever
+    // the drains before it did, the peers' data is read fresh
+    return ftar::KSignal{d->sig_cnt, d->sig_flag, ++d->sig_tag, 1u, gate_word(d, d->gate_seq), 2u * d->gate_seq,
+                         d->sig_flag + 32, d->gate_ticks};
+}
+
 // The TreeBatch of fdev_tree_batch(_gated): the grid (0 = a tree beyond the workgroup
 // budget, or nothing to do when B->nt == 0), link and HBM bytes.
 static int build_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
@@ -584,27 +612,16 @@ int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src
                           const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag, int *gated)
 {
     *gated = 0;
-    // a fenced marker or an unsignalled launch would have to drain behind the closed gate
-    if (!d->flag_sync || d->profiling || d->gate_pending || d->unsignalled || d->force_fence) return 0;
+    if (!can_gate(d, 1)) return 0;
     ftar::TreeBatch B;
     unsigned grid = 0;
     double link, hbm;
     int rc = build_batch(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, &B, &grid, &link, &hbm);
-    if (rc || grid == 0 || grid > d->flag_max) return rc;
-    d->gate_link = link; // counted when the gate opens to run it
-    d->gate_hbm = hbm;
-    d->pre_gate_any = d->signalled > 0;
-    d->pre_gate_tag = d->sig_tag;
-    d->gate_seq++;
-    // the workgroups invalidate their caches once the gate opens (acquire = 1): whatever
-    // the drains before it did, the peers' data is read fresh
-    B.sig = ftar::KSignal{d->sig_cnt, d->sig_flag, ++d->sig_tag, 1u, d->sig_flag + 16, 2u * d->gate_seq,
-                          d->sig_flag + 32, d->gate_ticks};
-    d->signalled++;
+    if (rc || !can_gate(d, grid)) return rc;
+    B.sig = arm_gate(d, link, hbm);
     hipError_t e = ftar::launch_tree_batch(dtype, op, nsrc, B, grid, d->stream);
     if (e != hipSuccess) return set_err(e, "tree_batch_kernel launch (gated)");
     d->gate_pending = 1;
-    d->after_gate = 0;
     *gated = 1;
     return 0;
 }
@@ -612,7 +629,7 @@ int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src
 int fdev_gate_open(ftar_dev *d, int skip)
 {
     if (!d->gate_pending) return 0;
-    __atomic_store_n(d->sig_flag + 16, 2u * d->gate_seq + (skip ? 1u : 0u), __ATOMIC_RELEASE);
+    __atomic_store_n(gate_word(d, d->gate_seq), 2u * d->gate_seq + (skip ? 1u : 0u), __ATOMIC_RELEASE);
     if (!skip) {
         d->ctr.link_bytes += d->gate_link;
         d->ctr.hbm_bytes += d->gate_hbm;
@@ -660,6 +677,43 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
 int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     return run_on(d, d->stream, dtype, op, segs, nseg, tag);
+}
+
+int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int *gated)
+{
+    *gated = 0;
+    size_t es = esize_of(dtype);
+    if (es == 0 || op < 0 || op >= ftar::kNumOps || nseg < 0 || nseg > FDEV_MAX_SEGS || tag < 0 || tag >= FDEV_NTAGS) {
+        snprintf(g_err, sizeof(g_err), "fdev_run_gated: bad arguments");
+        return 13;
+    }
+    ftar::SegIn in[FDEV_MAX_SEGS];
+    double link = 0, hbm = 0;
+    for (int i = 0; i < nseg; i++) {
+        in[i].kind = segs[i].kind == FDEV_COPY ? ftar::kCopy : ftar::kReduce;
+        in[i].out = segs[i].out;
+        in[i].x = segs[i].x;
+        in[i].y = segs[i].y;
+        in[i].n = segs[i].n;
+        in[i].out2 = segs[i].out2;
+        double b = (double)segs[i].n * (double)es;
+        int nread = segs[i].kind == FDEV_COPY ? 1 : 2;
+        int nremote = ((segs[i].remote & FDEV_REMOTE_X) ? 1 : 0) +
+                      ((segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) ? 1 : 0);
+        int rout = (segs[i].remote & FDEV_REMOTE_OUT) ? 1 : 0;
+        link += b * (nremote + rout);
+        hbm += b * (1 - rout + nread - nremote + (segs[i].out2 ? 1 : 0));
+    }
+    ftar::KSegList L;
+    unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
+    if (!can_gate(d, grid)) return 0;
+    L.nt_store = nt_store();
+    L.sig = arm_gate(d, link, hbm);
+    hipError_t e = ftar::launch_segments(dtype, op, L, grid, d->stream);
+    if (e != hipSuccess) return set_err(e, "segment_kernel launch (gated)");
+    d->gate_pending = 1;
+    *gated = 1;
+    return 0;
 }
 
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
@@ -712,6 +766,7 @@ int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int
 
 int fdev_order_after(ftar_dev *d, void *user_stream)
 {
+    if (d->gate_pending) (void)fdev_gate_open(d, 1); // nothing waits behind a closed gate
     // an idle caller stream has nothing our kernels must wait for (its kernels completed,
     // their stores released to this device); queuing the wait costs ~1.3 us
     hipError_t q = hipStreamQuery((hipStream_t)user_stream);
@@ -778,11 +833,8 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
     int rc;
     if (d->gate_pending) {
         // a launch waits on its closed gate: drain what was queued before it (all of it
-        // signalled, fdev_tree_batch_gated checked), never a marker behind the gate
-        if (d->after_gate) {
-            snprintf(g_err, sizeof(g_err), "fdev_sync: work queued behind a closed gate");
-            return 13;
-        }
+        // signalled, the gated launch checked; nothing is queued behind it, see note_launch),
+        // never a marker behind the gate
         rc = d->pre_gate_any ? wait_signal(d, d->pre_gate_tag, poll, arg) : 0;
         d->need_acquire = 1;
         d->pre_gate_any = 0;
@@ -809,7 +861,8 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
         unsigned t = __atomic_load_n(d->sig_flag + 32, __ATOMIC_ACQUIRE);
         if (t) {
             __atomic_store_n(d->sig_flag + 32, 0u, __ATOMIC_RELAXED);
-            snprintf(g_err, sizeof(g_err), "gated launch %u: its gate stayed closed past the timeout", t / 2);
+            snprintf(g_err, sizeof(g_err), "gated launch %u: its gate stayed closed past the timeout (or was overtaken)",
+                     t / 2);
             return 101;
         }
     }
@@ -828,6 +881,7 @@ int fdev_busy(ftar_dev *d)
 
 int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg)
 {
+    if (d->gate_pending) (void)fdev_gate_open(d, 1); // the background stream follows the main one
     if (!d->bg) return harvest(d); // never used: nothing queued
     int rc = sync_stream(d, d->bg, poll, arg);
     if (rc) return rc;
@@ -903,6 +957,7 @@ int fdev_wait_h2d(ftar_dev *d, int slot, int (*poll)(void *), void *arg)
 
 int fdev_d2h_async(ftar_dev *d, void *dst, const void *src, size_t bytes)
 {
+    if (d->gate_pending) (void)fdev_gate_open(d, 1);
     int rc = ensure_pipe(d);
     if (rc) return rc;
     hipEvent_t e = get_event(d);
@@ -916,6 +971,7 @@ int fdev_d2h_async(ftar_dev *d, void *dst, const void *src, size_t bytes)
 
 int fdev_sync_d2h(ftar_dev *d, int (*poll)(void *), void *arg)
 {
+    if (d->gate_pending) (void)fdev_gate_open(d, 1);
     if (!d->d2h) return 0;
     HIPCHK(hipEventRecord(d->fence_d2h, d->d2h));
     return spin(d->fence_d2h, poll, arg);

@@ -85,13 +85,22 @@ struct ftar_comm {
     int redundancy;      /* FTAR_REDUNDANCY (default 0: the step-0 copy is never moved; a replay reads the dead rank's IN) */
     int mesh;            /* FTAR_MESH (default 1): one-hop Raben at power-of-two p without a spare */
     int push;            /* FTAR_PUSH (default 0): the mesh by remote stores -- 1 reduce-scatter, 2 both phases */
-    int gate;            /* FTAR_GATE (default 1): small one-shot launch queued ahead of its barrier, gated */
+    int gate;            /* FTAR_GATE (default 1): small exchange launches queued ahead of their barrier, gated */
     size_t oneshot_max;  /* FTAR_ONESHOT_MAX bytes: mesh Raben in one launch up to this size */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
     /* the step's last peer read (FTAR_LOOP_SECONDS re-pulls it into pad while it waits) */
     const void *pad_src;
     size_t pad_bytes;
     void *pad; /* local scratch of FTAR_PAD_BYTES, allocated on the first padded step */
+    /* A segment launch queued behind a gate (ftar_prelaunch): the segments it was planned
+     * with, to be compared with the step's own when it comes (ftar_run_gated_or). */
+    struct ftar_gplan {
+        int valid, dtype, op, tag, nseg;
+        fdev_seg segs[FDEV_MAX_SEGS];
+    } gplan;
+    /* the next step's predicted segments: ftar_xfer_step queues them gated right behind
+     * the current step's launch (set by the schedule, consumed by the transport) */
+    struct ftar_gplan gnext;
 };
 
 #define FTAR_PAD_BYTES ((size_t)16 << 20)
@@ -135,6 +144,12 @@ void ftar_sync_fatal(ftar_comm *c);
 int ftar_drain(ftar_comm *c);
 /* enqueue one segment kernel */
 int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+/* Queue a step's segment launch ahead of the barrier that readies its operands, behind a
+ * gate (fdev_run_gated); returns 1 if it was queued.  ftar_run_gated_or runs a step's
+ * segments: it opens the pending gate if that launch was planned with exactly these
+ * segments, else gives it up (skip) and launches them. */
+int ftar_prelaunch(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+void ftar_run_gated_or(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
 /* bookkeeping of every launch: the control slot's in-flight word (FTAR_INFLIGHT_*) and,
  * for a peer read (`remote` != NULL, `bytes` of it), the step's re-pull source */
 void ftar_note_launch(ftar_comm *c, const void *remote, size_t bytes);
@@ -209,6 +224,8 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
 /* after the step's agree returned `known`: re-pull stripes lost with relays that died
  * before the mid barrier, then one more (uniform) barrier */
 void ftar_xfer_repair(ftar_comm *c, const ftar_plan *p, int dtype, int op, ftar_xstate *st, uint64_t known);
+/* the segments of this rank's direct pulls in plan p, appended to segs[ns..]; returns ns */
+int ftar_xfer_direct_segs(ftar_comm *c, const ftar_plan *p, size_t es, fdev_seg *segs, int ns);
 double ftar_link_bytes(ftar_comm *c);
 int ftar_xfer_would_relay(ftar_comm *c, const ftar_plan *p, size_t es);
 

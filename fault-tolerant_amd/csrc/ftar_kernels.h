@@ -32,12 +32,13 @@ constexpr int kMaxIleave = 16; // vector pieces that can share the interleaved p
 // returns without touching memory; either way it signals.  A gate still closed after
 // gate_ticks of the wall clock (tens of seconds: the host never got past its barrier) is
 // taken as skip and reported through `err`, which the host checks after the drain.
+constexpr unsigned kGateSlots = 8; // gate words, used in turn (sig_flag[16 + seq % 8])
 struct KSignal {
     unsigned *cnt;  // device counter, agent-scope atomics; nullptr = no signal
     unsigned *flag; // pinned host word
     unsigned tag;
     unsigned acquire;
-    const unsigned *gate; // pinned host word; nullptr = not gated
+    const unsigned *gate; // pinned host word (slot gate_val / 2 % kGateSlots); nullptr = not gated
     unsigned gate_val;
     unsigned *err;        // pinned host word: set to gate_val on a gate timeout
     unsigned long long gate_ticks;

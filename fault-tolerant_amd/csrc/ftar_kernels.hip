@@ -145,6 +145,8 @@ __device__ __forceinline__ void signal_acquire(const KSignal &G)
 // The gate of a launch queued ahead of its barrier (KSignal): 1 = run, 0 = skip.  One
 // lane polls the host word with system-scope loads (uncached, over PCIe), sleeping
 // between polls; the workgroup learns the verdict through LDS.  Uniform over the launch.
+// Gates take turns over kGateSlots words (ftar_kernels.h): a workgroup that starts late
+// still finds its own verdict after the host has opened the next gate.
 __device__ __forceinline__ bool signal_gate(const KSignal &G)
 {
     if (!G.gate) return true;
@@ -162,9 +164,11 @@ __device__ __forceinline__ bool signal_gate(const KSignal &G)
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        // one gate at a time: the host arms the next only after this launch has drained,
-        // so the word holds our sequence, and its bit 0 is the verdict
-        go = (v == G.gate_val) ? 1u : 0u;
+        if ((v & ~1u) != G.gate_val) { // the slot already holds a later gate: never run blind
+            __hip_atomic_store(G.err, G.gate_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            v |= 1u;
+        }
+        go = (v & 1u) ? 0u : 1u;
     }
     __syncthreads();
     return go != 0;
@@ -250,9 +254,11 @@ __global__ __launch_bounds__(kBlock) void segment_kernel(KSegList L)
     const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     const BlockWork w = map_block(L, b);
     const KSeg &S = L.s[__builtin_amdgcn_readfirstlane(w.seg)];
-    signal_acquire(L.sig);
-    if (S.vec) vec_body<T, OP>(S, w.first, w.stride, L.nt_store);
-    else scalar_body<T, OP>(S, w.first, w.stride);
+    if (signal_gate(L.sig)) {
+        signal_acquire(L.sig);
+        if (S.vec) vec_body<T, OP>(S, w.first, w.stride, L.nt_store);
+        else scalar_body<T, OP>(S, w.first, w.stride);
+    }
     signal_done(L.sig);
 }
 

@@ -580,12 +580,13 @@ static int rb_oneshot(rb_ctx *x, const void *sbuf, void *rbuf)
             ftar_note_launch(c, src[k], B.n[k / p] * x->es);
             break;
         }
-    int go = x->gated && memcmp(&B, &x->gplan, sizeof(B)) == 0;
-    if (x->gated) { /* the queued launch runs now, or returns untouched and is replaced */
-        fdev_gate_open(c->dev, !go);
-        if (!go) c->stats.gated_skips++;
-        x->gated = 0;
-    }
+    /* the queued launch runs now, or returns untouched and is replaced (also when another
+     * launch has given it up meanwhile) */
+    int pending = x->gated && fdev_gate_pending(c->dev);
+    int go = pending && memcmp(&B, &x->gplan, sizeof(B)) == 0;
+    if (x->gated && !go) c->stats.gated_skips++;
+    if (pending) fdev_gate_open(c->dev, !go);
+    x->gated = 0;
     if (!go && fdev_tree_batch(c->dev, x->dtype, x->op, src, p, B.remote, B.out, B.n, p, FDEV_TAG_STEP0)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);

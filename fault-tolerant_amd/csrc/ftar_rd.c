@@ -60,6 +60,50 @@ static void run1(rd_ctx *x, int kind, void *out, const void *a, const void *b, i
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
+/* Every active rank's pull at the step of `distance` (recursive_doubling.c:35-49): middle
+ * steps src = dst + src (Reduce_local(dst, src)), the last step dst = src + dst
+ * (Reduce_local(src, dst)) -- the pulled operand first.  This rank reads its accumulator
+ * from buffer `cur` and writes the other ping-pong buffer (returned); a partner's
+ * accumulator is where it published it, or in buffer `pred` (>= 0) when the plan is made
+ * ahead of the barrier that publishes it (every rank's buffers alternate alike). */
+static int rd_plan(rd_ctx *x, int distance, int cur, int pred, ftar_plan *P)
+{
+    ftar_comm *c = x->c;
+    int last = (distance * 2 >= x->nactive);
+    int i = index_of(x->active, x->nactive, c->wrank);
+    int out = (cur == WS_W) ? WS_T : WS_W;
+    ftar_plan_clear(P);
+    for (int a = 0; a < x->nactive; a++) {
+        int cr = ftar_comm_rank_of(c, x->active[a]);
+        int pw = x->active[a ^ distance];
+        ftar_pull *pl = &P->pull[cr][0];
+        *pl = (ftar_pull){FDEV_REDUCE, last, pw, pred >= 0 ? pred : peer_cur(x, pw), 0, 0, 0, (int64_t)x->count, 0};
+        if (a == i) {
+            pl->dst_buf = out;
+            pl->x_buf = cur;
+            pl->to_uout = last; /* the result also lands in dst (no final copy) */
+        }
+        P->npull[cr] = 1;
+    }
+    return out;
+}
+
+/* The segments of this rank's step at `distance` planned ahead (rd_plan with `pred`), into
+ * g; 0 if that step would be relayed (never queued ahead) or this rank pulls nothing. */
+static int rd_plan_ahead(rd_ctx *x, int distance, int cur, int pred, int tag, struct ftar_gplan *g)
+{
+    ftar_plan P;
+    rd_plan(x, distance, cur, pred, &P);
+    g->valid = 0;
+    if (ftar_xfer_would_relay(x->c, &P, x->es)) return 0;
+    g->nseg = ftar_xfer_direct_segs(x->c, &P, x->es, g->segs, 0);
+    g->dtype = x->dtype;
+    g->op = x->op;
+    g->tag = tag;
+    g->valid = g->nseg > 0;
+    return g->valid;
+}
+
 /* pull the accumulator of original rank `from` into a free buffer of this rank */
 static void restore_from(rd_ctx *x, int from)
 {
@@ -194,10 +238,9 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
      * step) the partner may still be reading IN. */
     const char *s0 = (const char *)src, *d0 = (const char *)dst;
     int disjoint = s0 + bytes <= d0 || d0 + bytes <= s0;
-    if (!ftar_stage_input(c, src, bytes, disjoint)) run1(x, FDEV_COPY, c->ws[WS_IN], src, NULL, 0, FDEV_TAG_LOCAL);
-    ftar_drain(c);
+    int staged = !ftar_stage_input(c, src, bytes, disjoint);
+    if (staged) run1(x, FDEV_COPY, c->ws[WS_IN], src, NULL, 0, FDEV_TAG_LOCAL);
     x->cur = WS_IN;
-    publish_cur(x);
 
     /* Data + reduce_pow2 (recursive_doubling.c:118-130, util.c:3-34) */
     int size = c->size;
@@ -206,6 +249,19 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     for (int i = 0; i < pp; i++) x->active[i] = c->order[i];
     x->ninactive = size - pp;
     for (int i = pp; i < size; i++) x->inactive[i - pp] = c->order[i];
+    /* Small calls at a power of two (no pre-step): each step's launch is queued ahead of the
+     * barrier that readies its operands, behind a gate (ftar_prelaunch) -- step 0's right
+     * behind the staging copy (every rank stages a small input, so the partners' inputs
+     * will be in their IN), step s + 1's behind step s's (the accumulators alternate W, T,
+     * W, ... on every rank).  The step then runs it only if its own plan, made after the
+     * barrier, is the same (ftar_xfer_step); a recovery in between makes it a plain launch. */
+    int ahead = c->gate && staged && x->ninactive == 0 && pp >= 2 && bytes <= c->stage_max && !c->copy_engine;
+    if (ahead && rd_plan_ahead(x, 1, WS_IN, WS_IN, FDEV_TAG_STEP0, &c->gnext)) {
+        c->gnext.valid = 0;
+        ftar_prelaunch(c, c->gnext.dtype, c->gnext.op, c->gnext.segs, c->gnext.nseg, c->gnext.tag);
+    }
+    ftar_drain(c);
+    publish_cur(x);
     uint64_t involved = 0; /* ranks with a pre-step exchange (errors there are fatal) */
     for (int r = 0; r < x->ninactive; r++) involved |= (1ull << x->active[r]) | (1ull << x->inactive[r]);
 
@@ -238,25 +294,12 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     for (int distance = 1; distance < x->nactive; distance *= 2, iter++) {
         int last = (distance * 2 >= x->nactive);
         int i = index_of(x->active, x->nactive, me);
-        int out = (x->cur == WS_W) ? WS_T : WS_W;
-        /* every active rank's pull (ftar_xfer stripes it over relays when large):
-         * middle steps src = dst + src (:48, Reduce_local(dst, src)), last step
-         * dst = src + dst (:44, Reduce_local(src, dst)) -- the pulled operand first */
+        /* every active rank's pull (ftar_xfer stripes it over relays when large) */
         ftar_plan P;
         ftar_xstate xs;
-        ftar_plan_clear(&P);
-        for (int a = 0; a < x->nactive; a++) {
-            int cr = ftar_comm_rank_of(c, x->active[a]);
-            int pw = x->active[a ^ distance];
-            ftar_pull *pl = &P.pull[cr][0];
-            *pl = (ftar_pull){FDEV_REDUCE, last, pw, peer_cur(x, pw), 0, 0, 0, (int64_t)count, 0};
-            if (a == i) {
-                pl->dst_buf = out;
-                pl->x_buf = x->cur;
-                pl->to_uout = last; /* the result also lands in dst (no final copy) */
-            }
-            P.npull[cr] = 1;
-        }
+        int out = rd_plan(x, distance, x->cur, -1, &P);
+        /* the next step's launch, queued gated behind this one's (see `ahead`) */
+        if (ahead && i >= 0 && !last) rd_plan_ahead(x, distance * 2, out, out, FDEV_TAG_STEP, &c->gnext);
         ftar_maybe_die(c, FTAR_PH_LOOP, iter, FTAR_PT_BEFORE);
         ftar_enter(c);
         int skip = 0;

@@ -199,6 +199,16 @@ void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int n
     }
 }
 
+int ftar_xfer_direct_segs(ftar_comm *c, const ftar_plan *p, size_t es, fdev_seg *segs, int ns)
+{
+    int me = ftar_my_comm_rank(c);
+    for (int u = 0; u < p->npull[me]; u++) {
+        const ftar_pull *pl = &p->pull[me][u];
+        segs[ns++] = own_seg(c, pl, pl->off, pl->n, at(ftar_buf(c, pl->src, pl->src_buf), pl->off, es), es);
+    }
+    return ns;
+}
+
 void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag, int skip, int kphase, int kstep,
                     const fdev_seg *extra, int nextra, ftar_xstate *xs)
 {
@@ -210,12 +220,15 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
     int ns = 0;
     for (int i = 0; i < nextra; i++) segs[ns++] = extra[i];
     if (!ftar_xfer_would_relay(c, p, es)) { /* direct pull of the whole window */
-        if (!skip)
-            for (int u = 0; u < p->npull[me]; u++) {
-                const ftar_pull *pl = &p->pull[me][u];
-                segs[ns++] = own_seg(c, pl, pl->off, pl->n, at(ftar_buf(c, pl->src, pl->src_buf), pl->off, es), es);
-            }
-        if (ns) ftar_run_pulls(c, dtype, op, segs, ns, tag, 0);
+        if (!skip) ns = ftar_xfer_direct_segs(c, p, es, segs, ns);
+        /* a launch queued for this step ahead of its barrier runs if it was planned with
+         * these very segments (ftar_run_gated_or), else it is replaced */
+        if (!c->copy_engine && (c->gplan.valid || fdev_gate_pending(c->dev))) ftar_run_gated_or(c, dtype, op, segs, ns, tag);
+        else if (ns) ftar_run_pulls(c, dtype, op, segs, ns, tag, 0);
+        if (c->gnext.valid) { /* the next step's launch, queued gated behind this one */
+            c->gnext.valid = 0;
+            ftar_prelaunch(c, c->gnext.dtype, c->gnext.op, c->gnext.segs, c->gnext.nseg, c->gnext.tag);
+        }
         ftar_launched(c, kphase, kstep); /* FTAR_PT_DURING: our pulls and the partner's in flight */
         if (ns) ftar_drain(c);
         ftar_exchange_done(c);
@@ -224,6 +237,11 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
     }
     xs->relayed = 1;
     c->stats.relayed_steps++;
+    c->gnext.valid = 0; /* relayed steps are never queued ahead (their first launch gives up any gate) */
+    if (c->gplan.valid) {
+        c->gplan.valid = 0;
+        c->stats.gated_skips++;
+    }
     int R[FTAR_MAX_RANKS], rel[FTAR_MAX_RANKS];
     int nr = receivers(c, p, R);
     /* phase 1: own stripe 0 + relay duties */

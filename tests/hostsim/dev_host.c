@@ -26,15 +26,18 @@ struct ftar_dev {
     int device;
     int profiling;
     fdev_counters ctr;
-    /* a gated batch (fdev_tree_batch_gated): held until its gate opens, run then unless
-     * skipped; anything queued meanwhile is a protocol error the next drain reports */
-    int gate_pending, after_gate;
+    /* a gated launch (fdev_tree_batch_gated / fdev_run_gated): held until its gate opens,
+     * run then unless skipped; any other launch meanwhile gives it up first (opened as
+     * skip), as the GPU build does */
+    int gate_pending;
     struct {
-        int dtype, op, nsrc, ntree, tag;
+        int batch; /* 1: a tree batch, 0: segments */
+        int dtype, op, nsrc, ntree, tag, nseg;
         const void *src[FDEV_MAX_BATCH * FDEV_MAX_BATCH];
         unsigned remote[FDEV_MAX_BATCH];
         void *out[FDEV_MAX_BATCH];
         size_t n[FDEV_MAX_BATCH];
+        fdev_seg segs[FDEV_MAX_SEGS];
     } gated;
     uint64_t gates_run, gates_skipped;
 };
@@ -220,7 +223,7 @@ static size_t esz(int dt) { return (dt == 0 || dt == 1) ? 4 : 8; }
 
 int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
-    if (d->gate_pending) d->after_gate = 1;
+    if (d->gate_pending) fdev_gate_open(d, 1);
     for (int k = 0; k < nseg; k++) {
         const fdev_seg *s = &segs[k];
         if (s->kind == FDEV_COPY) {
@@ -264,7 +267,7 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
                   void *const *more, int nmore, size_t n, int tag)
 {
     if (!(nsrc == 2 || nsrc == 4 || nsrc == 8 || nsrc == 16)) return 13;
-    if (d->gate_pending) d->after_gate = 1;
+    if (d->gate_pending) fdev_gate_open(d, 1);
     switch (dtype) {
     case 0: TREE(int32_t, op_i32); break;
     case 1: TREE(float, op_f32); break;
@@ -296,16 +299,22 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
     return 0;
 }
 
-/* host-sim: every batch can be gated (FTAR_HOSTSIM_GATE=0 turns it off, as a GPU whose
+/* host-sim: every launch can be gated (FTAR_HOSTSIM_GATE=0 turns it off, as a GPU whose
  * launch could not be); held, and run when the gate opens */
+static int can_gate(const ftar_dev *d)
+{
+    const char *e = getenv("FTAR_HOSTSIM_GATE");
+    return !(e && !atoi(e)) && !d->profiling && !d->gate_pending;
+}
+
 int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
                           const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
                           int *gated)
 {
     *gated = 0;
-    const char *e = getenv("FTAR_HOSTSIM_GATE");
-    if ((e && !atoi(e)) || d->profiling || d->gate_pending) return 0;
+    if (!can_gate(d)) return 0;
     if (!(nsrc == 2 || nsrc == 4 || nsrc == 8) || ntree < 1 || ntree > FDEV_MAX_BATCH) return 13;
+    d->gated.batch = 1;
     d->gated.dtype = dtype;
     d->gated.op = op;
     d->gated.nsrc = nsrc;
@@ -316,7 +325,22 @@ int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src
     memcpy(d->gated.out, out, sizeof(void *) * (size_t)ntree);
     memcpy(d->gated.n, n, sizeof(size_t) * (size_t)ntree);
     d->gate_pending = 1;
-    d->after_gate = 0;
+    *gated = 1;
+    return 0;
+}
+
+int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int *gated)
+{
+    *gated = 0;
+    if (!can_gate(d)) return 0;
+    if (nseg < 0 || nseg > FDEV_MAX_SEGS) return 13;
+    d->gated.batch = 0;
+    d->gated.dtype = dtype;
+    d->gated.op = op;
+    d->gated.tag = tag;
+    d->gated.nseg = nseg;
+    memcpy(d->gated.segs, segs, sizeof(fdev_seg) * (size_t)nseg);
+    d->gate_pending = 1;
     *gated = 1;
     return 0;
 }
@@ -330,6 +354,7 @@ int fdev_gate_open(ftar_dev *d, int skip)
         return 0;
     }
     d->gates_run++;
+    if (!d->gated.batch) return fdev_run(d, d->gated.dtype, d->gated.op, d->gated.segs, d->gated.nseg, d->gated.tag);
     return fdev_tree_batch(d, d->gated.dtype, d->gated.op, d->gated.src, d->gated.nsrc, d->gated.remote, d->gated.out,
                            d->gated.n, d->gated.ntree, d->gated.tag);
 }
@@ -345,7 +370,7 @@ int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg) { return poll ? po
 
 int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int remote, int tag)
 {
-    if (d->gate_pending) d->after_gate = 1;
+    if (d->gate_pending) fdev_gate_open(d, 1);
     memmove(dst, src, bytes);
     if (remote) d->ctr.link_bytes += (double)bytes;
     d->ctr.launches[tag]++;
@@ -356,10 +381,6 @@ int fdev_order_after(ftar_dev *d, void *s) { return 0; }
 
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 {
-    if (d->after_gate) { /* the GPU build refuses this drain too (it would wait behind the gate) */
-        snprintf(g_err, sizeof(g_err), "fdev_sync: work queued behind a closed gate");
-        return 13;
-    }
     if (poll) return poll(arg);
     return 0;
 }

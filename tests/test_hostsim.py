@@ -432,40 +432,54 @@ def test_oneshot_device_buffers(hostsim, oracle, p, mode):
                 assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
+@pytest.mark.parametrize("algo", ["raben", "rd"])
 @pytest.mark.parametrize("p", [2, 4, 8])
 @pytest.mark.parametrize("gate", ["1", "0"])
-def test_oneshot_gated_launch(hostsim, oracle, p, gate):
-    """The small one-shot launch is queued ahead of the barrier behind a gate (FTAR_GATE,
-    default on) and runs when the gate opens: one gated launch per call and rank, none
-    replaced, same bits; FTAR_GATE=0 launches after the barrier as before."""
+def test_gated_launches(hostsim, oracle, algo, p, gate):
+    """Small calls at a power of two queue their exchange launches ahead of the barrier
+    that readies the operands, behind a gate (FTAR_GATE, default on): Raben's one-shot
+    launch (one per call), every RD step's (log2 p per call: step 0 behind the staging
+    copy, step s + 1 behind step s); none replaced, same bits.  FTAR_GATE=0 launches after
+    the barriers."""
     ins = oracle.random_inputs(p, 1031, seed=p + 970)
-    o = oracle.rabenseifner(ins)
-    r = H.run_probe("raben", ins, iters=3, backend="hostsim", env_extra={"FTAR_GATE": gate})
+    o = _fn(oracle, algo)(ins)
+    r = H.run_probe(algo, ins, iters=3, backend="hostsim", env_extra={"FTAR_GATE": gate})
     assert r.returncode == 0, r.stderr[-1000:]
+    per_call = (1 if algo == "raben" else p.bit_length() - 1) if gate == "1" else 0
     for w in range(p):
         for it in range(3):
-            assert r.status[w][it][0] == 0 and r.status[w][it][9] == 1, r.status[w][it]
-            assert r.status[w][it][10:12] == ((1, 0) if gate == "1" else (0, 0)), r.status[w][it]
+            assert r.status[w][it][0] == 0, r.status[w][it]
+            assert algo == "rd" or r.status[w][it][9] == 1, r.status[w][it]
+            assert r.status[w][it][10:12] == (per_call, 0), r.status[w][it]
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
+@pytest.mark.parametrize("algo", ["raben", "rd"])
 @pytest.mark.parametrize("p", [2, 4])
-def test_oneshot_gated_launch_replaced_when_a_peer_reads_in_place(hostsim, oracle, p):
+def test_gated_launch_replaced_when_a_peer_reads_in_place(hostsim, oracle, algo, p):
     """A peer that lets its send buffer be read in place (here: its own FTAR_STAGE_MAX=0)
-    moves its input away from the staged IN the gated launch was planned on: after the
+    moves its input away from the staged IN a gated launch was planned on: after the
     inputs are resolved the plans differ, the gated launch is skipped (returns untouched)
     and a fresh one runs -- same bits."""
     ins = oracle.random_inputs(p, 1031, seed=p + 980)
-    o = oracle.rabenseifner(ins)
+    o = _fn(oracle, algo)(ins)
     env = {"FTAR_PROBE_RANK_ENV": "1:FTAR_STAGE_MAX=0"}  # host entry: sbuf = the exportable staging
-    r = H.run_probe("raben", ins, iters=2, backend="hostsim", env_extra=env)
+    r = H.run_probe(algo, ins, iters=2, backend="hostsim", env_extra=env)
     assert r.returncode == 0, r.stderr[-1000:]
+    L = p.bit_length() - 1
     for w in range(p):
         for it in range(2):
             st = r.status[w][it]
-            assert st[0] == 0 and st[9] == 1, st
-            # rank 1 reads nothing staged by itself: no gate; every other rank gated, then replaced
-            assert st[10:12] == ((0, 0) if w == 1 else (1, 1)), (w, st)
+            assert st[0] == 0, st
+            # rank 1 stages nothing: no gate.  Raben: every other rank's one-shot reads rank
+            # 1's input -> replaced.  RD: only rank 0 reads rank 1's input (its step-0 partner)
+            if w == 1:
+                want = (0, 0)
+            elif algo == "raben":
+                want = (1, 1)
+            else:
+                want = (L, 1 if w == 0 else 0)
+            assert st[10:12] == want, (w, st)
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
