@@ -54,7 +54,8 @@ def main():
         for name, fn, limit, gate in (("raben_oneshot", comm.allreduce_rabenseifner, 1 << 20, 1),
                                       ("raben_oneshot_nogate", comm.allreduce_rabenseifner, 1 << 20, 0),
                                       ("raben_mesh", comm.allreduce_rabenseifner, 0, 1),
-                                      ("rd", comm.recursive_doubling, 0, 1)):
+                                      ("rd", comm.recursive_doubling, 0, 1),
+                                      ("rd_nogate", comm.recursive_doubling, 0, 0)):
             comm.set_option(ftar.OPT_ONESHOT_MAX, limit)
             comm.set_option(ftar.OPT_GATE, gate)
             for _ in range(5):
