@@ -39,3 +39,17 @@ def test_xgmi_probe_patterns_virtual(n):
     assert set(d["patterns"]) == {"pull1", "push1", "pull1_bidir", "push1_bidir", "sdma1_bidir", "pull_all",
                                   "push_all"}, d
     assert all(p["ok"] and p["ms"] > 0 for p in d["patterns"].values()), d
+
+
+def test_gate_probe():
+    """tools/gate_probe.hip drives the product's gated segment kernel alone: a gate opened
+    as go copies and one opened as skip leaves the output untouched (both signal); a gate
+    never opened gives up after its timeout and reports it; workgroups that find a later
+    sequence in their gate word skip and report -- never a blind run, never a hang."""
+    cp = subprocess.run([os.path.join(ROOT, "tools", "_build", "gate_probe")], capture_output=True, text=True,
+                        timeout=120)
+    lines = [ln for ln in cp.stdout.splitlines() if ln.startswith("{")]
+    assert lines, cp.stdout[-1000:] + cp.stderr[-1000:]
+    d = json.loads(lines[-1])
+    assert cp.returncode == 0 and d["ok"], d
+    assert 90 <= d["timeout_ms"] < 2000, d

@@ -17,6 +17,7 @@
 #   sweep      tools/size_sweep.py with 2 / 4 / 8 ranks on GPU 0
 #   e2e        host-buffer Raben end to end: chunk pipeline on / off, zero copy (1 / 2 / 4 ranks)
 #   latency    tools/latency_probe.py with 2 / 4 / 8 ranks on GPU 0 (gated one-shot vs not)
+#   gateprobe  tools/gate_probe.hip: the gated launch alone (latency hidden, go / skip, timeout, overtaken)
 #   syncprobe  tools/sync_probe.hip: device round trip of one step
 #   cpubase    tools/cpu_schedule_bench.py on this box's host cores
 #   xgmi       tools/xgmi_probe.hip: one link / all peers, pull / push / copy engines (loopback on one GPU)
@@ -122,6 +123,10 @@ if has latency; then
         "$OUT/latency_${n}ranks.json" > "$OUT/latency_${n}ranks.log" 2>&1
     rc=$?; tail -c 400 "$OUT/latency_${n}ranks.log"; echo; stop_on_fault $rc latency_$n
   done
+fi
+if has gateprobe; then
+  timeout -k 10 120 tools/_build/gate_probe > "$OUT/gate_probe.json" 2>&1
+  rc=$?; cat "$OUT/gate_probe.json"; stop_on_fault $rc gateprobe
 fi
 if has syncprobe; then
   timeout -k 10 120 tools/_build/sync_probe > "$OUT/sync_probe.json" 2>&1
