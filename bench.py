@@ -1223,7 +1223,10 @@ def multi(args):
                 if time_left() < 15:
                     sizes["truncated_at_bytes"] = 4 * n
                     break
-                steps, warm = (20, 3) if n <= (1 << 22) else (5, 2)
+                # small calls: a long warm-up, so the timed calls see a GPU and host cores that
+                # are past their idle power states (a cold start measured 2-3x the per-call
+                # time in one-GPU rehearsals, profiles/r03/README.md)
+                steps, warm = (100, 50) if 4 * n <= (1 << 20) else (20, 3) if n <= (1 << 22) else (5, 2)
                 row = {"bytes": 4 * n}
                 for name, fn, extra in (("raben", comm.allreduce_rabenseifner, None),
                                         ("raben_no_oneshot", comm.allreduce_rabenseifner, 0),
@@ -1240,6 +1243,11 @@ def multi(args):
 
                     try:
                         row[name + "_us"] = round(quick(call, steps=steps, warmup=warm) * 1e6, 2)
+                        if 4 * n in (4, 65536):  # where a small call's time goes (max over ranks)
+                            row[name + "_split_us"] = {
+                                "drain": round(timed.breakdown["stream_drain_wait_ms"] * 1e3, 2),
+                                "agree_barrier": round(timed.breakdown["agree_barrier_wait_ms"] * 1e3, 2),
+                                "gated_launches": comm.last_stats().gated_launches}
                     finally:
                         comm.set_option(ftar.OPT_ONESHOT_MAX, oneshot_max)
                 if z is not None:

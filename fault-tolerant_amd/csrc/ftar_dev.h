@@ -131,8 +131,11 @@ int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, 
 int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int remote, int tag);
 /* Spin until the background stream drained. */
 int fdev_sync_bg(ftar_dev *d, int (*poll)(void *), void *arg);
-/* Make the rank's stream wait for everything queued on `user_stream` (hipStream_t). */
+/* Order the rank's work after everything queued on `user_stream` (hipStream_t): nothing to
+ * do if it is idle, else the host waits for it (never a marker queued on the caller's
+ * stream).  fdev_user_host_waits counts the calls that waited. */
 int fdev_order_after(ftar_dev *d, void *user_stream);
+int fdev_user_host_waits(const ftar_dev *d);
 /* Spin (busy, the process stays in R state) until the stream drained.  `poll` is
  * called between queries; a nonzero return aborts the wait with that value. */
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg);

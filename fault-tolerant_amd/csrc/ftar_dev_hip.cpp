@@ -129,7 +129,6 @@ struct ftar_dev {
     int signalled;         // ... with one
     int need_acquire;      // the last drain was a signal: no marker has invalidated the caches since
     int force_fence;       // the next drain must be a fenced marker (peers read caller memory in place)
-    int waited_user;       // a wait on the caller's stream was queued since the last drain
     // A launch queued ahead of its barrier (fdev_tree_batch_gated / fdev_run_gated): its
     // workgroups wait on a gate word (sig_flag[16 + seq % 8]) until fdev_gate_open; a gate
     // that timed out (or was found overtaken) is reported in sig_flag[32].
@@ -140,6 +139,7 @@ struct ftar_dev {
     unsigned pre_gate_tag; // ... the last of them
     unsigned long long gate_ticks; // wall-clock ticks before a closed gate counts as timed out
     double gate_link, gate_hbm;    // the gated launch's bytes (counted if it runs)
+    int user_host_waits;           // calls that found the caller's stream busy and waited for it
 };
 
 extern "C" {
@@ -185,9 +185,10 @@ int fdev_open(int device, ftar_dev **out)
         d->sig_cnt = nullptr;
         d->sig_flag = nullptr;
         d->sig_tag = 0;
-        d->unsignalled = d->signalled = d->need_acquire = d->force_fence = d->waited_user = 0;
+        d->unsignalled = d->signalled = d->need_acquire = d->force_fence = 0;
         d->gate_seq = 0;
         d->gate_pending = d->gate_verify = d->pre_gate_any = 0;
+        d->user_host_waits = 0;
         d->pre_gate_tag = 0;
         int khz = 0; // wall clock of the kernels (s_memrealtime), 100 MHz on CDNA
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
@@ -767,19 +768,25 @@ int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int
 int fdev_order_after(ftar_dev *d, void *user_stream)
 {
     if (d->gate_pending) (void)fdev_gate_open(d, 1); // nothing waits behind a closed gate
-    // an idle caller stream has nothing our kernels must wait for (its kernels completed,
-    // their stores released to this device); queuing the wait costs ~1.3 us
-    hipError_t q = hipStreamQuery((hipStream_t)user_stream);
+    // An idle caller stream has nothing our kernels must wait for (its kernels completed,
+    // their stores released to this device).  A busy one is waited for on the host, never
+    // by queuing a GPU-side dependency: an event recorded on the caller's stream is a
+    // marker there, which the NEXT call's hipStreamQuery then finds pending (the runtime
+    // reports completion of the caller's stream with a lag), so the wait was queued again
+    // on every call -- and a cross-queue wait behind a marker on an otherwise idle queue
+    // cost 30-50 us per call on one MI355X (tools/_exp_nullq.hip, profiles/r03/nullq/).
+    // The call blocks until its own kernels are done anyway; waiting for the caller's
+    // pending work first costs nothing extra.
+    hipStream_t s = (hipStream_t)user_stream;
+    hipError_t q = hipStreamQuery(s);
     if (q == hipSuccess) return 0;
     if (q != hipErrorNotReady) (void)hipGetLastError();
-    d->waited_user = 1;
-    hipEvent_t e = get_event(d);
-    if (!e) return set_err(hipErrorOutOfMemory, "hipEventCreate");
-    HIPCHK(hipEventRecord(e, (hipStream_t)user_stream));
-    HIPCHK(hipStreamWaitEvent(d->stream, e, 0));
-    d->event_pool.push_back(e); // safe: the wait was captured at enqueue time
+    d->user_host_waits++;
+    HIPCHK(hipStreamSynchronize(s));
     return 0;
 }
+
+int fdev_user_host_waits(const ftar_dev *d) { return d->user_host_waits; }
 
 static int harvest(ftar_dev *d);
 
@@ -838,12 +845,12 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
         rc = d->pre_gate_any ? wait_signal(d, d->pre_gate_tag, poll, arg) : 0;
         d->need_acquire = 1;
         d->pre_gate_any = 0;
-        d->unsignalled = d->waited_user = d->force_fence = 0;
+        d->unsignalled = d->force_fence = 0;
         d->signalled = 1; // the gated launch, drained after its gate opens
         if (rc) return rc;
         return harvest(d);
     }
-    if (!d->unsignalled && !d->signalled && !d->waited_user && !d->force_fence) {
+    if (!d->unsignalled && !d->signalled && !d->force_fence) {
         rc = 0; // nothing queued since the last drain
     } else if (!d->unsignalled && d->signalled && !d->force_fence) {
         // only signalled launches: each workgroup released its stores at system scope before
@@ -854,7 +861,7 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
         rc = sync_stream(d, d->stream, poll, arg);
         d->need_acquire = 0;
     }
-    d->unsignalled = d->signalled = d->waited_user = d->force_fence = 0;
+    d->unsignalled = d->signalled = d->force_fence = 0;
     if (rc) return rc;
     if (d->gate_verify) { // the gated launch has completed: did its gate time out?
         d->gate_verify = 0;

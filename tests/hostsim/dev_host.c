@@ -378,6 +378,7 @@ int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int
 }
 
 int fdev_order_after(ftar_dev *d, void *s) { return 0; }
+int fdev_user_host_waits(const ftar_dev *d) { return 0; }
 
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 {
