@@ -114,6 +114,12 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
 int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
                           const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
                           int *gated);
+/* The same, with this rank's staging copy folded in ahead of the gate: the launch first
+ * copies stage_n elements from stage_src to stage_dst (all of it, whatever the gate
+ * says) and signals that; the drain before the barrier waits for that signal. */
+int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
+                                 const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
+                                 void *stage_dst, const void *stage_src, size_t stage_n, int *gated);
 /* fdev_run's segment kernel queued behind a gate, on the same terms. */
 int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int *gated);
 /* Open the pending gate (no-op without one).  skip = 1: the gated launch does nothing.

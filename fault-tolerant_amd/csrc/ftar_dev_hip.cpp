@@ -609,8 +609,9 @@ static int build_batch(ftar_dev *d, int dtype, int op, const void *const *src, i
     return 0;
 }
 
-int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
-                          const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag, int *gated)
+int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
+                                 const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
+                                 void *stage_dst, const void *stage_src, size_t stage_n, int *gated)
 {
     *gated = 0;
     if (!can_gate(d, 1)) return 0;
@@ -619,12 +620,35 @@ int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src
     double link, hbm;
     int rc = build_batch(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, &B, &grid, &link, &hbm);
     if (rc || !can_gate(d, grid)) return rc;
+    unsigned stage_tag = 0;
+    if (stage_dst && stage_n) {
+        stage_tag = ++d->sig_tag; // the launch raises the flag twice: staged, then done
+        d->ctr.hbm_bytes += 2.0 * (double)stage_n * (double)esize_of(dtype);
+    }
     B.sig = arm_gate(d, link, hbm);
+    if (stage_tag) {
+        B.sig.stage_src = stage_src;
+        B.sig.stage_dst = stage_dst;
+        B.sig.stage_n = stage_n;
+        B.sig.stage_es = (unsigned)esize_of(dtype);
+        B.sig.stage_tag = stage_tag;
+        B.sig.stage_cnt = d->sig_cnt + 16; // its own counter, 64 B from the completion counter
+        d->pre_gate_any = 1;               // the drain before the barrier waits for "staged"
+        d->pre_gate_tag = stage_tag;
+    }
     hipError_t e = ftar::launch_tree_batch(dtype, op, nsrc, B, grid, d->stream);
     if (e != hipSuccess) return set_err(e, "tree_batch_kernel launch (gated)");
     d->gate_pending = 1;
     *gated = 1;
     return 0;
+}
+
+int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
+                          const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
+                          int *gated)
+{
+    return fdev_tree_batch_staged_gated(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, nullptr, nullptr, 0,
+                                        gated);
 }
 
 int fdev_gate_open(ftar_dev *d, int skip)

@@ -42,6 +42,17 @@ struct KSignal {
     unsigned gate_val;
     unsigned *err;        // pinned host word: set to gate_val on a gate timeout
     unsigned long long gate_ticks;
+    // Optional staging phase BEFORE the gate (a gated launch that also stages this rank's
+    // input for its peers, saving the separate staging launch): every workgroup copies its
+    // share of stage_n elements of stage_es bytes from stage_src to stage_dst, releases its
+    // stores at system scope and counts itself in stage_cnt; the last one stores stage_tag
+    // into `flag` -- the host's signal that the input is staged, before it opens the gate.
+    const void *stage_src;
+    void *stage_dst;
+    size_t stage_n;
+    unsigned stage_es;
+    unsigned stage_tag;
+    unsigned *stage_cnt;  // device counter (agent scope)
 };
 
 struct KSeg {

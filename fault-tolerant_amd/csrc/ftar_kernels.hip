@@ -142,6 +142,38 @@ __device__ __forceinline__ void signal_acquire(const KSignal &G)
     }
 }
 
+// Staging phase of a gated launch (KSignal stage_*): this rank's input copied into its
+// exported buffer, element by element (any alignment; a small launch), then released and
+// signalled to the host -- all before the gate, which the host opens only after it saw the
+// signal and the peers' barrier.  The grid is small (<= FTAR_FLAG_MAX_BLOCKS workgroups), so
+// every workgroup is resident while the others wait at the gate.
+template <typename E>
+__device__ __forceinline__ void stage_copy(const KSignal &G)
+{
+    const E *s = (const E *)G.stage_src;
+    E *d = (E *)G.stage_dst;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < G.stage_n; i += stride) d[i] = s[i];
+}
+
+__device__ __forceinline__ void signal_stage(const KSignal &G)
+{
+    if (!G.stage_dst) return;
+    if (G.stage_es == 8) stage_copy<unsigned long long>(G);
+    else stage_copy<unsigned>(G);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // system scope: the staged input to HBM for the peers
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(G.stage_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gridDim.x - 1) {
+            __hip_atomic_store(G.stage_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(G.flag, G.stage_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // The gate of a launch queued ahead of its barrier (KSignal): 1 = run, 0 = skip.  One
 // lane polls the host word with system-scope loads (uncached, over PCIe), sleeping
 // between polls; the workgroup learns the verdict through LDS.  Uniform over the launch.
@@ -351,6 +383,7 @@ __global__ __launch_bounds__(kBlock) void tree_batch_kernel(TreeBatch B)
     const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     int k = 0;
     while (k + 1 < B.nt && b >= B.first[k + 1]) k++;
+    signal_stage(B.sig);
     if (signal_gate(B.sig)) {
         signal_acquire(B.sig);
         tree_body<T, OP, P>(B.t[k], b - B.first[k], B.first[k + 1] - B.first[k]);

@@ -551,14 +551,17 @@ static void rb_oneshot_plan(rb_ctx *x, const void *sbuf, void *rbuf, struct rb_b
  * overlaps the staging drain and the barrier.  The plan assumes every peer stages its
  * input (this rank did, so the size is the same everywhere); rb_oneshot re-plans after
  * the inputs are resolved and skips the gated launch if anything differs. */
-static void rb_oneshot_prelaunch(rb_ctx *x, const void *sbuf, void *rbuf)
+static void rb_oneshot_prelaunch(rb_ctx *x, const void *sbuf, void *rbuf, void *stage_dst)
 {
     ftar_comm *c = x->c;
     x->gated = 0;
     if (!c->gate) return;
     rb_oneshot_plan(x, sbuf, rbuf, &x->gplan);
-    if (fdev_tree_batch_gated(c->dev, x->dtype, x->op, x->gplan.src, x->adjsize, x->gplan.remote, x->gplan.out,
-                              x->gplan.n, x->adjsize, FDEV_TAG_STEP0, &x->gated)) {
+    /* stage_dst: this rank's staging copy (sbuf -> IN) rides in the same launch, ahead of
+     * the gate -- one launch per call instead of two */
+    if (fdev_tree_batch_staged_gated(c->dev, x->dtype, x->op, x->gplan.src, x->adjsize, x->gplan.remote,
+                                     x->gplan.out, x->gplan.n, x->adjsize, FDEV_TAG_STEP0, stage_dst, sbuf,
+                                     stage_dst ? x->count : 0, &x->gated)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
@@ -708,10 +711,16 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
     } else if (x->oneshot) {
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
-        run_copy(x, IN, sbuf, (int64_t)count, 0, FDEV_TAG_LOCAL);
         /* small inputs are staged by every rank (ftar_stage_input): the launch's operands
-         * are known before the barrier */
-        if (bytes <= c->stage_max) rb_oneshot_prelaunch(x, sbuf, rbuf);
+         * are known before the barrier, and the staging copy can ride in it */
+        if (bytes <= c->stage_max) {
+            rb_oneshot_prelaunch(x, sbuf, rbuf, IN);
+            if (x->gated) ftar_note_launch(c, NULL, 0); /* the staging phase is in flight */
+        }
+        if (!x->gated) {
+            run_copy(x, IN, sbuf, (int64_t)count, 0, FDEV_TAG_LOCAL);
+            if (bytes <= c->stage_max) rb_oneshot_prelaunch(x, sbuf, rbuf, NULL);
+        }
     } else if (x->mesh) { /* peers pull every block of sbuf but this rank's own final one */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         int64_t b0 = x->rindex[x->steps - 1], b1 = b0 + x->rcount[x->steps - 1];

@@ -329,6 +329,16 @@ int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src
     return 0;
 }
 
+int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
+                                 const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
+                                 void *stage_dst, const void *stage_src, size_t stage_n, int *gated)
+{
+    *gated = 0;
+    if (!can_gate(d)) return 0;
+    if (stage_dst && stage_n) memmove(stage_dst, stage_src, stage_n * esz(dtype)); /* before the gate, always */
+    return fdev_tree_batch_gated(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, gated);
+}
+
 int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int *gated)
 {
     *gated = 0;
