@@ -578,12 +578,13 @@ static void note_segs(ftar_comm *c, int dtype, const fdev_seg *segs, int nseg)
         atomic_store_explicit(&c->job.shm->slot[c->wrank].inflight, FTAR_INFLIGHT_PULL, memory_order_release);
 }
 
-int ftar_prelaunch(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
+int ftar_prelaunch(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag, void *stage_dst,
+                   const void *stage_src, size_t stage_n)
 {
     int gated = 0;
     c->gplan.valid = 0;
     if (!c->gate || nseg <= 0 || nseg > FDEV_MAX_SEGS) return 0;
-    if (fdev_run_gated(c->dev, dtype, op, segs, nseg, tag, &gated)) {
+    if (fdev_run_gated(c->dev, dtype, op, segs, nseg, tag, stage_dst, stage_src, stage_n, &gated)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }

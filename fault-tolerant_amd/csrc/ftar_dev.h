@@ -120,8 +120,10 @@ int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src
 int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
                                  const unsigned *remote_mask, void *const *out, const size_t *n, int ntree, int tag,
                                  void *stage_dst, const void *stage_src, size_t stage_n, int *gated);
-/* fdev_run's segment kernel queued behind a gate, on the same terms. */
-int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int *gated);
+/* fdev_run's segment kernel queued behind a gate, on the same terms (stage_dst != NULL:
+ * with the staging phase folded in, as fdev_tree_batch_staged_gated). */
+int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, void *stage_dst,
+                   const void *stage_src, size_t stage_n, int *gated);
 /* Open the pending gate (no-op without one).  skip = 1: the gated launch does nothing.
  * Any other launch or stream wait queued while a gate is pending opens it as skip first
  * (nothing may wait behind a closed gate): a caller about to open its gate checks

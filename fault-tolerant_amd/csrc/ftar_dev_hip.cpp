@@ -704,7 +704,8 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
     return run_on(d, d->stream, dtype, op, segs, nseg, tag);
 }
 
-int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int *gated)
+int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, void *stage_dst,
+                   const void *stage_src, size_t stage_n, int *gated)
 {
     *gated = 0;
     size_t es = esize_of(dtype);
@@ -733,7 +734,22 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
     if (!can_gate(d, grid)) return 0;
     L.nt_store = nt_store();
+    unsigned stage_tag = 0;
+    if (stage_dst && stage_n) {
+        stage_tag = ++d->sig_tag; // the launch raises the flag twice: staged, then done
+        d->ctr.hbm_bytes += 2.0 * (double)stage_n * (double)es;
+    }
     L.sig = arm_gate(d, link, hbm);
+    if (stage_tag) {
+        L.sig.stage_src = stage_src;
+        L.sig.stage_dst = stage_dst;
+        L.sig.stage_n = stage_n;
+        L.sig.stage_es = (unsigned)es;
+        L.sig.stage_tag = stage_tag;
+        L.sig.stage_cnt = d->sig_cnt + 16;
+        d->pre_gate_any = 1;
+        d->pre_gate_tag = stage_tag;
+    }
     hipError_t e = ftar::launch_segments(dtype, op, L, grid, d->stream);
     if (e != hipSuccess) return set_err(e, "segment_kernel launch (gated)");
     d->gate_pending = 1;

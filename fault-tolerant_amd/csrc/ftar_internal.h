@@ -148,7 +148,8 @@ int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, in
  * gate (fdev_run_gated); returns 1 if it was queued.  ftar_run_gated_or runs a step's
  * segments: it opens the pending gate if that launch was planned with exactly these
  * segments, else gives it up (skip) and launches them. */
-int ftar_prelaunch(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
+int ftar_prelaunch(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag, void *stage_dst,
+                   const void *stage_src, size_t stage_n);
 void ftar_run_gated_or(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
 /* bookkeeping of every launch: the control slot's in-flight word (FTAR_INFLIGHT_*) and,
  * for a peer read (`remote` != NULL, `bytes` of it), the step's re-pull source */

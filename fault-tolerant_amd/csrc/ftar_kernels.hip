@@ -286,6 +286,7 @@ __global__ __launch_bounds__(kBlock) void segment_kernel(KSegList L)
     const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x);
     const BlockWork w = map_block(L, b);
     const KSeg &S = L.s[__builtin_amdgcn_readfirstlane(w.seg)];
+    signal_stage(L.sig);
     if (signal_gate(L.sig)) {
         signal_acquire(L.sig);
         if (S.vec) vec_body<T, OP>(S, w.first, w.stride, L.nt_store);

@@ -239,7 +239,6 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     const char *s0 = (const char *)src, *d0 = (const char *)dst;
     int disjoint = s0 + bytes <= d0 || d0 + bytes <= s0;
     int staged = !ftar_stage_input(c, src, bytes, disjoint);
-    if (staged) run1(x, FDEV_COPY, c->ws[WS_IN], src, NULL, 0, FDEV_TAG_LOCAL);
     x->cur = WS_IN;
 
     /* Data + reduce_pow2 (recursive_doubling.c:118-130, util.c:3-34) */
@@ -256,10 +255,14 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
      * W, ... on every rank).  The step then runs it only if its own plan, made after the
      * barrier, is the same (ftar_xfer_step); a recovery in between makes it a plain launch. */
     int ahead = c->gate && staged && x->ninactive == 0 && pp >= 2 && bytes <= c->stage_max && !c->copy_engine;
+    int folded = 0; /* the staging copy rides in step 0's gated launch, ahead of its gate */
     if (ahead && rd_plan_ahead(x, 1, WS_IN, WS_IN, FDEV_TAG_STEP0, &c->gnext)) {
         c->gnext.valid = 0;
-        ftar_prelaunch(c, c->gnext.dtype, c->gnext.op, c->gnext.segs, c->gnext.nseg, c->gnext.tag);
+        folded = ftar_prelaunch(c, c->gnext.dtype, c->gnext.op, c->gnext.segs, c->gnext.nseg, c->gnext.tag,
+                                c->ws[WS_IN], src, count);
+        if (folded) ftar_note_launch(c, NULL, 0); /* the staging phase is in flight */
     }
+    if (staged && !folded) run1(x, FDEV_COPY, c->ws[WS_IN], src, NULL, 0, FDEV_TAG_LOCAL);
     ftar_drain(c);
     publish_cur(x);
     uint64_t involved = 0; /* ranks with a pre-step exchange (errors there are fatal) */

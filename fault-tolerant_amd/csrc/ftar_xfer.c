@@ -227,7 +227,7 @@ void ftar_xfer_step(ftar_comm *c, const ftar_plan *p, int dtype, int op, int tag
         else if (ns) ftar_run_pulls(c, dtype, op, segs, ns, tag, 0);
         if (c->gnext.valid) { /* the next step's launch, queued gated behind this one */
             c->gnext.valid = 0;
-            ftar_prelaunch(c, c->gnext.dtype, c->gnext.op, c->gnext.segs, c->gnext.nseg, c->gnext.tag);
+            ftar_prelaunch(c, c->gnext.dtype, c->gnext.op, c->gnext.segs, c->gnext.nseg, c->gnext.tag, NULL, NULL, 0);
         }
         ftar_launched(c, kphase, kstep); /* FTAR_PT_DURING: our pulls and the partner's in flight */
         if (ns) ftar_drain(c);

@@ -339,10 +339,12 @@ int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *con
     return fdev_tree_batch_gated(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, gated);
 }
 
-int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, int *gated)
+int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, void *stage_dst,
+                   const void *stage_src, size_t stage_n, int *gated)
 {
     *gated = 0;
     if (!can_gate(d)) return 0;
+    if (stage_dst && stage_n) memmove(stage_dst, stage_src, stage_n * esz(dtype)); /* before the gate, always */
     if (nseg < 0 || nseg > FDEV_MAX_SEGS) return 13;
     d->gated.batch = 0;
     d->gated.dtype = dtype;
