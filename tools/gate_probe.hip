@@ -10,6 +10,8 @@
 //               timeout word holds the gate's value and the flag is raised -- no hang
 //   overtaken : a gate whose word already holds a later sequence when its workgroups look
 //               (they started late): skip + the timeout word, never a blind run
+//   staged    : the staging phase ahead of the gate -- the staged data is there and signalled
+//               before the gate opens, the gated work only after
 // Prints one JSON line.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I fault-tolerant_amd/csrc tools/gate_probe.hip \
 //         fault-tolerant_amd/csrc/ftar_kernels.hip -o tools/_build/gate_probe
@@ -162,13 +164,41 @@ int main()
     CHK(hipMemcpy(o.data(), dst, n * 4, hipMemcpyDeviceToHost));
     bool overtaken_ok = oerr == 2u * seq && std::all_of(o.begin(), o.end(), [](float v) { return v == 0.f; });
 
+    // staged: the launch first stages n floats (into pinned host memory here, so the host can
+    // look without a runtime call) and raises the flag with the staging tag, then waits at
+    // its gate; the host sees the staged data before it opens the gate
+    float *hstage = nullptr, *hdst = nullptr; // both pinned: the host looks without a runtime call
+    CHK(hipHostMalloc((void **)&hstage, n * 4, hipHostMallocCoherent | hipHostMallocMapped));
+    CHK(hipHostMalloc((void **)&hdst, n * 4, hipHostMallocCoherent | hipHostMallocMapped));
+    memset(hstage, 0, n * 4);
+    memset(hdst, 0, n * 4);
+    CHK(hipDeviceSynchronize());
+    ++seq;
+    {
+        ftar::SegIn in{ftar::kCopy, hdst, src, nullptr, n, nullptr};
+        ftar::KSegList L;
+        unsigned grid = ftar::plan_segments(&in, 1, 4, 1 << 20, &L);
+        L.nt_store = 1;
+        const unsigned stage_tag = ++P.tag;
+        L.sig = ftar::KSignal{P.cnt, P.sig, ++P.tag, 1u, P.gate(seq), 2u * seq, P.err(), gate_ticks,
+                              src, hstage, n, 4u, stage_tag, P.cnt + 16};
+        CHK(ftar::launch_segments(ftar::kFloat32, ftar::kSum, L, grid, P.st));
+        P.wait_flag(stage_tag);
+    }
+    bool staged_before_gate = memcmp(hstage, h.data(), n * 4) == 0;
+    bool gated_not_run = std::all_of(hdst, hdst + n, [](float v) { return v == 0.f; }); // still at its gate
+    __atomic_store_n(P.gate(seq), 2u * seq, __ATOMIC_RELEASE);
+    P.wait_flag(P.tag);
+    CHK(hipStreamSynchronize(P.st));
+    bool staged_ok = staged_before_gate && gated_not_run && memcmp(hdst, h.data(), n * 4) == 0;
+
     printf("{\"tool\": \"gate_probe\", \"bytes\": %zu, \"workgroups\": 16, \"barrier_us\": 30, "
            "\"launch_after_barrier_to_flag_us\": %.2f, \"gate_open_to_flag_us\": %.2f, \"hidden_us\": %.2f, "
            "\"latency_runs_ok\": %s, \"go_ok\": %s, \"skip_ok\": %s, \"timeout_ok\": %s, \"timeout_ms\": %.1f, "
-           "\"overtaken_ok\": %s, \"ok\": %s}\n",
+           "\"overtaken_ok\": %s, \"staged_ok\": %s, \"ok\": %s}\n",
            n * 4, median(plain), median(gated), median(plain) - median(gated), lat_ok ? "true" : "false",
            go_ok ? "true" : "false", skip_ok ? "true" : "false", timeout_ok ? "true" : "false", timeout_ms,
-           overtaken_ok ? "true" : "false",
-           (lat_ok && go_ok && skip_ok && timeout_ok && overtaken_ok) ? "true" : "false");
-    return (lat_ok && go_ok && skip_ok && timeout_ok && overtaken_ok) ? 0 : 1;
+           overtaken_ok ? "true" : "false", staged_ok ? "true" : "false",
+           (lat_ok && go_ok && skip_ok && timeout_ok && overtaken_ok && staged_ok) ? "true" : "false");
+    return (lat_ok && go_ok && skip_ok && timeout_ok && overtaken_ok && staged_ok) ? 0 : 1;
 }
