@@ -828,6 +828,14 @@ void ftar_stats_begin(ftar_comm *c)
 
 void ftar_stats_end(ftar_comm *c)
 {
+    /* A gated launch still waiting at the end of the call (a recovery ended the loop before
+     * the step it was queued for): give it up now, rather than leave it to time out */
+    if (fdev_gate_pending(c->dev)) {
+        fdev_gate_open(c->dev, 1);
+        c->stats.gated_skips++;
+    }
+    c->gplan.valid = 0;
+    c->gnext.valid = 0;
     fdev_counters k;
     fdev_counters_get(c->dev, &k);
     c->stats.wall_s = now_s() - g_t0;
