@@ -203,8 +203,9 @@ typedef enum {
                                   of each block into the owner's HBM, the owner reduces locally), 2 = both
                                   phases (the owner's tree also stores its block into every peer; p <= 8),
                                   0 = remote loads (default) */
-    FTAR_OPT_GATE = 9          /* queue the small one-shot launch ahead of the barrier that readies its
-                                  operands, its workgroups waiting on a gate the barrier opens (0/1,
+    FTAR_OPT_GATE = 9          /* queue small exchange launches (Raben one-shot, RD steps) ahead of the
+                                  barrier that readies their operands, the staging copy folded into the
+                                  first, their workgroups waiting on a gate the barrier opens (0/1,
                                   default 1): the launch latency overlaps the wait for the peers */
 } ftar_option;
 
