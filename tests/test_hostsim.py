@@ -124,6 +124,44 @@ def test_repeated_calls_and_retargeted_comm(hostsim, oracle):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o2.outputs[i].view(np.uint32))
 
 
+@pytest.mark.parametrize("p", [4, 8])
+def test_rd_repeated_calls_after_recovery(hostsim, oracle, p):
+    """RD at a power of two queues every small step's launch ahead of its barrier (gates):
+    a recovery in call 0 re-targets the partners, so launches queued for the old plan are
+    given up (a gate still closed at the end of the call included); calls 1 and 2 on the
+    survivors are exact and gated again where the survivors are a power of two."""
+    inputs = oracle.random_inputs(p, 1031, seed=p + 21)
+    found = None
+    for v in range(p):
+        for st in range(p.bit_length() - 1):
+            for pt in (0, 2, 3):
+                ks = [(v, 1, st, pt)]
+                o1 = oracle.recursive_doubling(inputs, ks)
+                if not o1.aborted and len(o1.order_after) < p:
+                    found = ks, o1
+                    break
+            if found:
+                break
+        if found:
+            break
+    assert found, "no recovering RD kill"
+    kills, o1 = found
+    r = H.run_probe("rd", inputs, kills, iters=3, backend="hostsim")
+    assert not r.aborted, r.stderr[-1500:]
+    order = o1.order_after
+    o2 = oracle.recursive_doubling([inputs[w] for w in order])
+    for i, w in enumerate(order):
+        assert np.array_equal(r.outputs[w][0].view(np.uint32), o1.outputs[w].view(np.uint32)), w
+        assert r.status[w][0][10] >= 1, r.status[w][0]  # call 0 queued step 0 ahead of the kill
+        for it in (1, 2):
+            st = r.status[w][it]
+            assert st[0] == 0, st
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o2.outputs[i].view(np.uint32)), (w, it)
+            n = len(order)
+            if n & (n - 1) == 0:  # a power of two again: every step gated, none replaced
+                assert st[10:12] == (n.bit_length() - 1, 0), st
+
+
 def test_rd_after_raben_recovery(hostsim, oracle):
     """RD after a Raben recovery runs on the re-targeted comm order."""
     inputs = oracle.random_inputs(9, 777, seed=5)
