@@ -1309,6 +1309,8 @@ def multi(args):
 
     # IPC exports the runtime refused and the library re-allocated (expected 0)
     final["export_retries_max_over_ranks"] = int(max_over_ranks([float(comm.last_stats().export_retries)])[0])
+    # calls that found the caller's stream busy and waited for it on the host
+    final["user_stream_waits_max_over_ranks"] = int(max_over_ranks([float(comm.last_stats().user_stream_waits)])[0])
     line = build_line(transports, t_ref, k_ref)
     line.update(final)
     line["c5_single_kill"] = c5

@@ -45,7 +45,8 @@ class Stats(ctypes.Structure):
                 ("bg_kernel_ms", ctypes.c_double), ("sync_wait_s", ctypes.c_double),
                 ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int), ("relayed_steps", ctypes.c_int),
                 ("mesh_steps", ctypes.c_int), ("export_retries", ctypes.c_int),
-                ("gated_launches", ctypes.c_int), ("gated_skips", ctypes.c_int)]
+                ("gated_launches", ctypes.c_int), ("gated_skips", ctypes.c_int),
+                ("user_stream_waits", ctypes.c_int)]
 
 
 class Kill(ctypes.Structure):

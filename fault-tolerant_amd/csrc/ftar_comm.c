@@ -847,6 +847,7 @@ void ftar_stats_end(ftar_comm *c)
     c->stats.kernels += k.launches[0] + k.launches[1] + k.launches[2] + k.launches[3] + k.launches[4];
     c->stats.comm_size_after = c->size;
     c->stats.export_retries = fdev_export_retries(c->dev);
+    c->stats.user_stream_waits = fdev_user_host_waits(c->dev);
     ftar_inputs_done(c);
 }
 

@@ -234,6 +234,8 @@ typedef struct {
                                 re-allocated, cumulative since ftar_init (expected: 0) */
     int    gated_launches;   /* launches queued ahead of their barrier (FTAR_OPT_GATE) */
     int    gated_skips;      /* ... of them replaced after the barrier (a peer's input moved) */
+    int    user_stream_waits; /* calls that found the caller's stream busy and waited for it on the host,
+                                 cumulative since ftar_init */
 } ftar_stats;
 
 int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);
