@@ -121,16 +121,21 @@ def load_tool(name):
 
 
 def pmc_traffic(name):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_summary.json,
+    written by tools/pmc_summary.py from separate `--pmc` passes), and where that number comes
+    from: PMC counters need rocprofv3 around the process, so this run does not measure them --
+    `traffic_source` names the file, the entry and the commit / date it was measured at."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    src = {"measured_in_this_run": False, "file": "profiles/pmc_summary.json", "entry": name}
     if not os.path.exists(path):
-        return None
+        return None, dict(src, missing=True)
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(name, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(name, {})
     except (OSError, ValueError):
-        return None
+        return None, dict(src, unreadable=True)
+    src.update({k: e[k] for k in ("measured_at", "command", "counters") if k in e})
+    return e.get("hbm_bytes_per_launch"), src
 
 
 def cpu_baseline_local_reduce(min_seconds=10.0, max_passes=2000):
@@ -223,6 +228,7 @@ def single(args):
     _, k_same = region(min(args.steps, 100), 1)
     S = args.count * 4
     achieved = 3 * S / (k_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("reduce_local_c2_lds_rot" if args.variant == 1 else "reduce_local_c2_rot")
     out = {
         "metric": METRIC, "value": round(2 * S / (ms_step * 1e-3) / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
@@ -234,7 +240,7 @@ def single(args):
                               f"beyond the 256 MiB Infinity Cache)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic("reduce_local_c2_lds_rot" if args.variant == 1 else "reduce_local_c2_rot"),
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "reduce_lds_kernel<float,SUM>" if args.variant == 1 else "segment_kernel<float,SUM>",
                      "algorithmic_bytes_per_launch": 3 * S,
                      "kernel_ms": round(k_ms, 4),
@@ -329,10 +335,13 @@ def c5_leg(world, devices, count, ranks, deadline, calls=6, kill_call=2):
     fault job kills vrank 5 (original rank 6) in reduce-scatter step 1 of call `kill_call`,
     mid-exchange (its own pull kernel in flight, its partner's pull reading its HBM), a
     second one in allgather step 1 ("also AG step 1"; the last AG step when
-    there are only two).  Every job runs in both recovery shapes: the default (no step-0
-    redundancy copy; the replay reads the dead rank's step-0 half in its still-mapped IN)
-    and the reference's (FTAR_REDUNDANCY=1: the copy moves in every call and the replay
-    reads it, raben/rabenseifner.c:206-211).  The recovery shrinks the comm; the later
+    there are only two).  Every job runs in both recovery shapes: the library's default
+    (FTAR_REDUNDANCY auto: the reference's step-0 copy moves when the ranks span more than
+    one GPU, raben/rabenseifner.c:206-211; on one GPU it is elided and the replay reads the
+    dead rank's step-0 half in its still-mapped IN, DESIGN.md deviation 6) and the other one
+    (on the node the elided shape, opt-in FTAR_REDUNDANCY=0 -- its RS-kill job says whether a
+    dead process's memory stays readable across GPUs: `dead_input_cross_device`; on one GPU
+    the reference's copy, FTAR_REDUNDANCY=1).  The recovery shrinks the comm; the later
     calls run on the survivors.  Call 0 is the warm-up (workspace allocation, IPC
     imports).  Every job ends by `deadline` (killed past it)."""
     ftrun, exe = _ftrun_paths()
@@ -340,6 +349,7 @@ def c5_leg(world, devices, count, ranks, deadline, calls=6, kill_call=2):
     victim = 6 if ranks > 6 else ranks - 1
     ag_step = 1 if ranks >= 8 else 0  # a middle allgather step where there is one (L >= 3)
     env = _c5_env()
+    multi_gpu = len(set(devmap)) > 1
     res = {"ranks": ranks, "devmap": devmap, "count": count, "calls": calls,
            "kill": f"{victim}:1:1:3 in call {kill_call} (original rank {victim} = vrank {victim - 1}, reduce-scatter "
                    "step 1, mid-exchange)",
@@ -350,8 +360,8 @@ def c5_leg(world, devices, count, ranks, deadline, calls=6, kill_call=2):
         e = dict(env)
         if kill:
             e["FTAR_KILL"] = kill
-        if redundancy:
-            e["FTAR_REDUNDANCY"] = "1"
+        if redundancy is not None:
+            e["FTAR_REDUNDANCY"] = redundancy
         t0 = time.time()
         rem = left(deadline)
         if rem < 1.0:
@@ -370,7 +380,10 @@ def c5_leg(world, devices, count, ranks, deadline, calls=6, kill_call=2):
                              "comm_size_after": min((p["comm_size"] for p in per), default=None),
                              "result_ok": bool(per) and all(p["rc"] == 0 and p["uniform"] and p["value"] == want
                                                             for p in per)})
-        r = {"rc": rc, "survivors": len(lines), "job_wall_s": round(time.time() - t0, 2), "calls": per_call}
+        r = {"rc": rc, "survivors": len(lines), "job_wall_s": round(time.time() - t0, 2), "calls": per_call,
+             "aborted": "MPI_ABORT" in err,
+             "device_error": any(s in err for s in ("device error", "Memory access fault", "HSA_STATUS_ERROR")),
+             "step0_copy": lines[0].get("step0_copy") if lines else None}
         if to:
             r["timed_out"] = True
         if rc != 0 or not lines:
@@ -407,19 +420,31 @@ def c5_leg(world, devices, count, ranks, deadline, calls=6, kill_call=2):
         return s
 
     maybe_hang("c5", deadline)
-    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}"),
-                       ("fault_ag", f"{victim}:2:{ag_step}:3:{kill_call}")):
-        res[name] = job(kill, False)
+    jobs = (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}"), ("fault_ag", f"{victim}:2:{ag_step}:3:{kill_call}"))
+    for name, kill in jobs:
+        res[name] = job(kill, None)
     res.update(summarize(res["no_fault"], res["fault"], res["fault_ag"]))
-    ref = {"shape": "FTAR_REDUNDANCY=1: the step-0 copy of the partner's other half moves in every call and the RS "
-                    "replay reads it (raben/rabenseifner.c:206-211, raben/errhandler.c:106-200)"}
-    for name, kill in (("no_fault", None), ("fault", f"{victim}:1:1:3:{kill_call}"),
-                       ("fault_ag", f"{victim}:2:{ag_step}:3:{kill_call}")):
-        ref[name] = job(kill, True)
-    ref.update(summarize(ref["no_fault"], ref["fault"], ref["fault_ag"]))
-    res["recovery_shape"] = ("default: no step-0 redundancy copy; the RS replay reads the dead rank's step-0 half in "
-                             "its IN, still mapped by the peers (DESIGN.md 3, deviation 6)")
-    res["reference_shape"] = ref
+    copy_desc = ("the reference's step-0 copy of the partner's other half moves in every call and the RS replay reads "
+                 "it (raben/rabenseifner.c:206-211, raben/errhandler.c:106-200)")
+    elided_desc = ("no step-0 copy; the RS replay reads the dead rank's step-0 half in its IN, still mapped by the "
+                   "peers (DESIGN.md 3, deviation 6)")
+    res["recovery_shape"] = ("default (FTAR_REDUNDANCY auto): " + (copy_desc + " -- the ranks span GPUs" if multi_gpu
+                                                                   else elided_desc + " -- one GPU"))
+    other = {"shape": ("FTAR_REDUNDANCY=0 (opt-in): " + elided_desc) if multi_gpu else
+             ("FTAR_REDUNDANCY=1: " + copy_desc)}
+    for name, kill in jobs:
+        other[name] = job(kill, "0" if multi_gpu else "1")
+    other.update(summarize(other["no_fault"], other["fault"], other["fault_ag"]))
+    if multi_gpu:
+        # the premise of the elided shape, decided on the node: does a SIGKILLed rank's
+        # memory stay readable through its peers' mappings across GPUs?
+        f = other["fault"]
+        other["dead_input_cross_device"] = ("recovered" if other.get("recovered_rs") else "abort" if f.get("aborted")
+                                            else "fault" if f.get("device_error") or f.get("rc") else "wrong")
+        res["elided_shape"] = other
+        res["dead_input_cross_device"] = other["dead_input_cross_device"]
+    else:
+        res["reference_shape"] = other
     res["reference_leonardo_s"] = dict(REF_C5_S, note="clock() s per run incl. the whole MPI job, 460.6 MiB int32")
     return res
 
@@ -672,14 +697,32 @@ class Watchdog(threading.Thread):
         os._exit(0 if self.line is not None else 3)
 
 
+def _fraction(bound_s, t_s):
+    """A roofline fraction: the time bound over the measured time.  Above 1 (beyond timer
+    noise) the measurement beat its own bound -- the link price underestimates the fabric --
+    so no fraction is claimed: `frac` is null, the ratio is kept as `frac_raw`, `met` null."""
+    r = bound_s / t_s
+    if r > 1.02:
+        return {"frac": None, "frac_raw": round(r, 4), "met": None,
+                "bound_violated": "measured time below this bound: the link price is too low (see link_calibration)"}
+    return {"frac": round(r, 4), "met": r >= NORTH_STAR_FRAC}
+
+
 def north_star_block(world, S, t_head, transport, link_gbps, links, head_bytes_per_link, t_ref=None, rehearsal=False):
     """BASELINE.json north_star / SURVEY.md 8d: >= 70 % of the xGMI-bound roofline for the
-    device-resident Rabenseifner Allreduce of 256 MiB float32 at 8 GPUs.  SURVEY's roofline
-    is the FT schedule's data movement over one link per step, (2.5 - 2^(1-L)) S per rank
-    and direction (2.25 S at p = 8), priced at the calibrated single-link rate (B_link, both
-    directions loaded); the nominal 76.8 / 153.6 GB/s per direction are kept beside it as
-    assumptions.  Also priced: the bound of the schedule that ran (e.g. the one-hop mesh:
-    2 S / p over each of p - 1 links at once), which is the stricter yardstick."""
+    device-resident Rabenseifner Allreduce of 256 MiB float32 at 8 GPUs.
+
+    Every `frac` here is a time bound divided by the time of the schedule it bounds:
+      * `frac` / `met` (top level): the timed headline schedule against ITS OWN link bound --
+        e.g. the one-hop mesh moves 2 S / p over each of p - 1 links at once, so its bound
+        is (2 S / p) / B_link -- at the calibrated single-link rate B_link (both directions
+        loaded), the nominal 76.8 / SURVEY's 153.6 GB/s per direction beside it as assumptions;
+      * `reference_schedule_frac`: the reference's own data movement (pairwise, step by step,
+        step-0 full exchange: (2.5 - 2^(1-L)) S per rank and direction over one link per step,
+        2.25 S at p = 8 -- SURVEY.md 8d's roofline) timed in the same job, against that bound;
+      * `speedup_vs_survey_roofline`: SURVEY's FT roofline time over the headline time -- how
+        much faster the schedule that ran is than the reference's schedule could ever be on
+        one link per step.  A speed-up, never a fraction: it exceeds 1 by design."""
     L = world.bit_length() - 1
     ft_bytes = (2.5 - 2.0 ** (1 - L)) * S
     priced = {}
@@ -689,32 +732,38 @@ def north_star_block(world, S, t_head, transport, link_gbps, links, head_bytes_p
             continue
         t_roof = ft_bytes / (b * 1e9)
         t_sched = head_bytes_per_link / (b * 1e9)
-        row = {"link_GBps": round(b, 2), "t_roof_ms": round(t_roof * 1e3, 4),
-               "algbw_roof_GBps": round(S / t_roof / 1e9, 2),
-               "target_algbw_GBps": round(NORTH_STAR_FRAC * S / t_roof / 1e9, 2),
-               "frac": round(t_roof / t_head, 4), "met": t_roof / t_head >= NORTH_STAR_FRAC,
-               "schedule_t_roof_ms": round(t_sched * 1e3, 4), "schedule_frac": round(t_sched / t_head, 4)}
+        row = {"link_GBps": round(b, 2), "schedule_t_roof_ms": round(t_sched * 1e3, 4),
+               "schedule": _fraction(t_sched, t_head),
+               "survey_t_roof_ms": round(t_roof * 1e3, 4), "survey_algbw_roof_GBps": round(S / t_roof / 1e9, 2),
+               "survey_target_algbw_GBps": round(NORTH_STAR_FRAC * S / t_roof / 1e9, 2),
+               "speedup_vs_survey_roofline": round(t_roof / t_head, 4)}
         if t_ref:
-            row["reference_shape"] = {"frac": round(t_roof / t_ref, 4), "met": t_roof / t_ref >= NORTH_STAR_FRAC}
+            row["reference_schedule"] = _fraction(t_roof, t_ref)
         priced[tag] = row
     basis = "calibrated" if "calibrated" in priced else "survey_153.6_assumed"
     if rehearsal:  # every rank on one GPU: no link in the path, fractions would mix yardsticks
         for row in priced.values():
-            for k in ("frac", "met", "schedule_frac"):
-                row[k] = None
-            if "reference_shape" in row:
-                row["reference_shape"] = {"frac": None, "met": None}
-    out = {"target": f">= {NORTH_STAR_FRAC:.0%} of SURVEY.md 8d's xGMI roofline for FT Rabenseifner, 256 MiB float32 "
-                     f"SUM, 8 GPUs", "applies": world == 8, "n_gpus": world,
-           "roofline_definition": f"(2.5 - 2^(1-L)) S = {ft_bytes:.0f} B per rank and direction over one link per step "
-                                  "(the reference's FT schedule), at B_link",
+            row["schedule"] = {"frac": None, "met": None}
+            row["speedup_vs_survey_roofline"] = None
+            if "reference_schedule" in row:
+                row["reference_schedule"] = {"frac": None, "met": None}
+    b = priced[basis]
+    out = {"target": f">= {NORTH_STAR_FRAC:.0%} of the xGMI-bound roofline, FT Rabenseifner, 256 MiB float32 SUM, "
+                     f"8 GPUs", "applies": world == 8, "n_gpus": world,
+           "frac_definition": "headline schedule's own link bound / its measured time (bytes per link / B_link)",
            "schedule": transport, "schedule_bytes_per_link": head_bytes_per_link, "schedule_links": links,
            "algbw_GBps": round(S / t_head / 1e9, 2), "ms_per_step": round(t_head * 1e3, 4),
-           "basis": basis, "frac": priced[basis]["frac"], "met": priced[basis]["met"], "priced": priced,
-           "rehearsal": rehearsal}
+           "basis": basis, "frac": b["schedule"]["frac"], "met": b["schedule"]["met"],
+           "survey_roofline_definition": f"(2.5 - 2^(1-L)) S = {ft_bytes:.0f} B per rank and direction over one link "
+                                         "per step (the reference's FT schedule), at B_link",
+           "speedup_vs_survey_roofline": b["speedup_vs_survey_roofline"],
+           "priced": priced, "rehearsal": rehearsal}
+    if "bound_violated" in b["schedule"]:
+        out["bound_violated"] = b["schedule"]["bound_violated"]
     if t_ref:
         out["reference_shape_ms"] = round(t_ref * 1e3, 4)
-        out["reference_shape_met"] = priced[basis]["reference_shape"]["met"]
+        out["reference_schedule_frac"] = b["reference_schedule"]["frac"]
+        out["reference_schedule_met"] = b["reference_schedule"]["met"]
     return out
 
 
@@ -828,11 +877,13 @@ def multi(args):
     def quick(fn, steps=3, warmup=1):
         return timed(fn, steps, warmup)[0]
 
-    opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY, ftar.OPT_MESH, ftar.OPT_PUSH)
+    opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY, ftar.OPT_MESH, ftar.OPT_PUSH,
+            ftar.OPT_TREE_UNROLL)
+    pads = (0, 0, 0, 0, 0, 0, 1)  # PUSH off and one vector per tree lane unless named
     defaults = {o: comm.get_option(o) for o in opts}
 
     def set_opts(vals):
-        vals = tuple(vals) + (0,) * (len(opts) - len(vals))  # PUSH off unless named
+        vals = tuple(vals) + pads[len(vals):]
         for o, v in zip(opts, vals):
             comm.set_option(o, v)
 
@@ -875,21 +926,28 @@ def multi(args):
         # (mesh, relay, push): the mesh pulls the peers' parts of each block (remote loads)
         # or, mesh_push, has every rank store its parts into the owners (remote stores) --
         # which one the fabric moves faster is measured here, not assumed
+        # (mesh, relay, push, tree unroll)
         cands = {}
         if pow2 and comm.get_option(ftar.OPT_MESH):
-            cands["mesh"] = (1, 1, 0)
-            cands["mesh_push"] = (1, 1, 1)  # remote stores in the reduce-scatter
+            cands["mesh"] = (1, 1, 0, 1)
+            if world in (4, 8):
+                # 2 / 4 vectors per lane and source in the tree kernel: more loads in flight
+                # per lane when the p - 1 sources are remote (xGMI latency) -- the one-GPU A/B
+                # saw HBM contention only, so the node decides
+                cands["mesh_u2"] = (1, 1, 0, 2)
+                cands["mesh_u4"] = (1, 1, 0, 4)
+            cands["mesh_push"] = (1, 1, 1, 1)  # remote stores in the reduce-scatter
             if world <= 8:
-                cands["mesh_push2"] = (1, 1, 2)  # ... and in the allgather
+                cands["mesh_push2"] = (1, 1, 2, 1)  # ... and in the allgather
         if world >= 3 and comm.get_option(ftar.OPT_RELAY):
-            cands["relay2hop"] = (0, 1, 0)
-        cands["direct"] = (0, 0, 0)
+            cands["relay2hop"] = (0, 1, 0, 1)
+        cands["direct"] = (0, 0, 0, 1)
+        sel_opts = (ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH, ftar.OPT_TREE_UNROLL)
         if len(cands) > 1:
             times, inexact, failed = {}, [], {}
-            for name, (m, r, pu) in cands.items():
-                comm.set_option(ftar.OPT_MESH, m)
-                comm.set_option(ftar.OPT_RELAY, r)
-                comm.set_option(ftar.OPT_PUSH, pu)
+            for name, vals in cands.items():
+                for o, v in zip(sel_opts, vals):
+                    comm.set_option(o, v)
                 try:
                     maybe_fail(f"select:{name}")
                     if max_over_ranks([exact_ok(comm.allreduce_rabenseifner, trials=(0,))])[0]:
@@ -900,11 +958,11 @@ def multi(args):
                     failed[name] = str(e)[-200:]
             if times:
                 chosen = min(times, key=times.get)
-                for o, v in zip((ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH), cands[chosen]):
+                for o, v in zip(sel_opts, cands[chosen]):
                     comm.set_option(o, v)
             else:  # every one failed: keep the defaults, exact_on_node reports it
                 chosen = None
-                for o in (ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH):
+                for o in sel_opts:
                     comm.set_option(o, defaults[o])
             selection = {f"{k}_ms": round(t * 1e3, 4) for k, t in times.items()}
             selection.update({"chosen": chosen, "inexact": inexact, "failed": failed})
@@ -918,8 +976,10 @@ def multi(args):
     oneshot = comm.last_stats().mesh_steps == 1  # the mesh's one-launch form (p = 2, small vectors)
     push_opt = int(comm.get_option(ftar.OPT_PUSH))
     pushed = meshed and not oneshot and push_opt != 0
+    unroll = int(comm.get_option(ftar.OPT_TREE_UNROLL)) if world in (4, 8) else 1
     transport = "mesh-oneshot" if oneshot else ("mesh-push2" if push_opt == 2 and world <= 8 else "mesh-push") \
-        if pushed else "mesh" if meshed else "relay2hop" if relayed else "direct"
+        if pushed else (f"mesh-u{unroll}" if unroll > 1 else "mesh") if meshed else "relay2hop" if relayed else "direct"
+    keep = bool(comm.last_stats().step0_copy)  # the headline call moved the reference's step-0 copy
     chosen_opts = {o: comm.get_option(o) for o in opts}
 
     L = world.bit_length() - 1
@@ -932,7 +992,6 @@ def multi(args):
     # over r-1 links); a direct step moves it over one link.
     ft_bytes = (2.5 - 2.0 ** (1 - L)) * S
     classic = 2 * (1 - 2.0 ** -L) * S
-    keep = world != r_core or comm.get_option(ftar.OPT_REDUNDANCY) != 0
     sched_bytes = ft_bytes if keep else classic
     if oneshot:
         per_link = float(S)  # every peer's whole vector over its own link (= 2 S / p at p = 2)
@@ -975,6 +1034,10 @@ def multi(args):
                         "(power-of-two p, no spare)",
         "mesh": "Rabenseifner, one-hop mesh: reduce-scatter as one tree kernel over p-1 peer pulls, allgather as "
                 "one multi-source pull (power-of-two p, no spare; same reduction tree as recursive halving)",
+        "mesh-u2": "Rabenseifner, one-hop mesh, tree kernel with 2 vectors per lane and source (more remote loads in "
+                   "flight), allgather as one multi-source pull (power-of-two p, no spare; same tree)",
+        "mesh-u4": "Rabenseifner, one-hop mesh, tree kernel with 4 vectors per lane and source (more remote loads in "
+                   "flight), allgather as one multi-source pull (power-of-two p, no spare; same tree)",
         "mesh-push": "Rabenseifner, one-hop mesh, push form: every rank stores its part of each block into the "
                      "owner's HBM (p-1 remote-store copies in one launch), each owner reduces its block locally in the "
                      "same tree, allgather as one multi-source pull (power-of-two p, no spare)",
@@ -1032,7 +1095,9 @@ def multi(args):
                          # HBM bytes per launch from PMC exist for the one-GPU rehearsal only
                          # (every peer on this device); on the node the peer reads hit the
                          # peers' HBM and the counters of one device miss them
-                         "traffic": pmc_traffic(f"mesh_tree_p{world}_rehearsal") if rehearsal and meshed
+                         "traffic": pmc_traffic(f"mesh_tree_p{world}_rehearsal")[0] if rehearsal and meshed
+                         and not oneshot else None,
+                         "traffic_source": pmc_traffic(f"mesh_tree_p{world}_rehearsal")[1] if rehearsal and meshed
                          and not oneshot else None,
                          "traffic_note": "PMC counters of a peer-reading kernel are per device; not collected on "
                                          "the 8-GPU node (profiles/pmc_summary.json has the one-GPU rehearsal's: "
@@ -1103,36 +1168,94 @@ def multi(args):
         cks_want = ((world * (world - 1) // 2) % 17) * args.count
         return err, {"raben": cks_raben == cks_want, "rd": cks_rd == cks_want}
 
+    # The small-call mechanisms -- completion signalled by the kernels themselves
+    # (<= 64 workgroups), inputs staged below FTAR_STAGE_MAX, launches queued behind gates
+    # (Raben one-shot below FTAR_ONESHOT_MAX, RD steps) -- each has a size threshold near
+    # 1 MiB; the checks straddle it, gated and ungated, for both schedules.
+    EXACT_SIZES = (("4B", 1), ("4KiB", 1024), ("64KiB", 16384), ("1MiB-16B", 262140), ("1MiB", 262144),
+                   ("1MiB+16B", 262148), ("4MiB", 1 << 20))
+    small_fallback = {}
+
     def exact_leg():
-        # Exactness of every transport on this node (helpers above the selection)
-        checks = [("chosen", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, None),
-                  ("reference_shape", (0, 0, 0, 1, 0), comm.allreduce_rabenseifner, None),
-                  ("rd", [chosen_opts[o] for o in opts], comm.recursive_doubling, None),
-                  ("chosen_64KiB", [chosen_opts[o] for o in opts], comm.allreduce_rabenseifner, 16384)]
+        # Exactness of every transport and mechanism on this node (helpers above the selection)
+        base = [chosen_opts[o] for o in opts]
+        raben_fn, rd_fn = comm.allreduce_rabenseifner, comm.recursive_doubling
+        # (name, option values, function, count or None = the job's, extra options)
+        checks = [("chosen", base, raben_fn, None, {}),
+                  ("reference_shape", (0, 0, 0, 1, 0), raben_fn, None, {}),
+                  ("rd", base, rd_fn, None, {}),
+                  ("chosen_64KiB", base, raben_fn, 16384, {})]
+        small = []  # the checks of the small-call mechanisms (the fallback below reruns them)
+        for label, n in EXACT_SIZES:
+            if n > args.count:
+                continue
+            for algo, fn in (("raben", raben_fn), ("rd", rd_fn)):
+                for gate in (1, 0):
+                    small.append((f"{algo}_{label}_{'gated' if gate else 'ungated'}", base, fn, n,
+                                  {ftar.OPT_GATE: gate}))
+        checks += small
         if not args.no_variants:
-            checks += [(name, vals, comm.allreduce_rabenseifner, None) for name, vals in
-                       (("mesh", (1, 1, 0, 0, 1)), ("mesh_push", (1, 1, 0, 0, 1, 1)),
-                        ("mesh_push2", (1, 1, 0, 0, 1, 2)), ("relay2hop", (1, 1, 0, 0, 0)),
-                        ("direct", (0, 1, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)))
+            checks += [(name, vals, raben_fn, None, {}) for name, vals in
+                       (("mesh", (1, 1, 0, 0, 1)), ("mesh_u2", (1, 1, 0, 0, 1, 0, 2)), ("mesh_u4", (1, 1, 0, 0, 1, 0, 4)),
+                        ("mesh_push", (1, 1, 0, 0, 1, 1)), ("mesh_push2", (1, 1, 0, 0, 1, 2)),
+                        ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)))
                        if pow2 or not name.startswith("mesh")]
-            checks += [("rd_relay", (1, 1, 0, 0, 0), comm.recursive_doubling, None),
-                       ("rd_direct", (0, 1, 0, 0, 0), comm.recursive_doubling, None)]
-        comm.set_profiling(False)
-        fails = []
-        try:
-            for name, vals, fn, n in checks:
+            if pow2:
+                checks += [(name, vals, raben_fn, min(16384, args.count), {}) for name, vals in
+                           (("mesh_push_64KiB", (1, 1, 0, 0, 1, 1)), ("mesh_push2_64KiB", (1, 1, 0, 0, 1, 2)),
+                            ("mesh_u4_64KiB", (1, 1, 0, 0, 1, 0, 4)))]
+            checks += [("rd_relay", (1, 1, 0, 0, 0), rd_fn, None, {}),
+                       ("rd_direct", (0, 1, 0, 0, 0), rd_fn, None, {})]
+        gate0 = comm.get_option(ftar.OPT_GATE)
+        flag0 = comm.get_option(ftar.OPT_FLAG_SYNC)
+
+        def run(cks, extra=None):
+            fails = []
+            for name, vals, fn, n, more in cks:
                 set_opts(vals)
                 if name == "rd" and rd_selection:  # the transport the RD timing chose
                     comm.set_option(ftar.OPT_RELAY, int(rd_selection["chosen"] == "relay2hop"))
+                for o, v in {**more, **(extra or {})}.items():
+                    comm.set_option(o, v)
+                maybe_fail(f"exact:{name}")
                 fails.append(exact_ok(fn, n=n))
+                comm.set_option(ftar.OPT_GATE, gate0)
+            return max_over_ranks(fails) if fails else []
+
+        comm.set_profiling(False)
+        try:
+            fails = run(checks)
+            exact = {"inputs": "integer-valued float32 in [-1024, 1024), new per trial, 2 trials per check; "
+                               "expected sum regenerated on every rank (exact in any order)",
+                     "all_exact": all(f == 0 for f in fails)}
+            exact.update({name: f == 0 for (name, _, _, _, _), f in zip(checks, fails)})
+            # A small-call check that is not exact says which mechanism broke: rerun the failing
+            # ones with the gates off, then also with the kernels' completion flags off (fenced
+            # marker drains), and keep the first setting under which all of them are exact for
+            # the rest of the job -- the size sweep is timed with it.
+            bad = [c for c, f in zip(checks, fails) if f]
+            if any(c in small for c in bad):
+                tried = []
+                chosen_setting = None
+                for label, extra in (("gate=0", {ftar.OPT_GATE: 0}),
+                                     ("gate=0,flag_sync=0", {ftar.OPT_GATE: 0, ftar.OPT_FLAG_SYNC: 0})):
+                    f2 = run(bad, extra)  # every failing check (a small mesh call is gated too)
+                    comm.set_option(ftar.OPT_FLAG_SYNC, flag0)
+                    still = [c[0] for c, f in zip(bad, f2) if f]
+                    tried.append({"setting": label, "exact": not still, "still_inexact": still})
+                    if not any(c in small for c, f in zip(bad, f2) if f):
+                        chosen_setting = (label, extra, not still)
+                        break
+                small_fallback.update({"failed": [c[0] for c in bad], "tried": tried,
+                                       "setting": chosen_setting[0] if chosen_setting else None})
+                if chosen_setting:
+                    for o, v in chosen_setting[1].items():
+                        comm.set_option(o, v)
+                exact["small_call_fallback"] = small_fallback
+                exact["all_exact_after_fallback"] = bool(chosen_setting and chosen_setting[2])
         finally:
             set_opts([chosen_opts[o] for o in opts])
             comm.set_profiling(True)
-        fails = max_over_ranks(fails)
-        exact = {"inputs": "integer-valued float32 in [-1024, 1024), new per trial, 2 trials per transport; "
-                           "expected sum regenerated on every rank (exact in any order)",
-                 "all_exact": all(f == 0 for f in fails)}
-        exact.update({name: f == 0 for (name, _, _, _), f in zip(checks, fails)})
         return exact
 
     def ref_shape_leg():
@@ -1213,7 +1336,10 @@ def multi(args):
         # transport, next to RCCL's all_reduce on the same sizes: the FT/vendor curve of the
         # reference's compare campaign (slurm/test_compare.slurm:27-50, check_compare.py),
         # plus the fixed cost per call and the one-shot threshold (FTAR_ONESHOT_MAX)
-        sizes = {}
+        # timed with the small-call setting exact_on_node kept (a fallback if a gated or
+        # flag-signalled check was not exact on this node)
+        sizes = {"small_call_setting": small_fallback.get("setting") or "default (gates, flag-signalled drains)",
+                 "gate": comm.get_option(ftar.OPT_GATE), "flag_sync": comm.get_option(ftar.OPT_FLAG_SYNC)}
         comm.set_profiling(False)  # no kernel events: the plain per-call cost
         oneshot_max = comm.get_option(ftar.OPT_ONESHOT_MAX)
         z = x.clone() if nccl else None

@@ -29,6 +29,9 @@ OPT_OVERLAP, OPT_RELAY, OPT_RELAY_MIN, OPT_LOOP_SECONDS, OPT_COPY_ENGINE, OPT_RE
 OPT_ONESHOT_MAX = 7
 OPT_PUSH = 8
 OPT_GATE = 9
+OPT_FLAG_SYNC = 10
+OPT_TREE_UNROLL = 11
+REDUNDANCY_NEVER, REDUNDANCY_ALWAYS, REDUNDANCY_AUTO = 0, 1, 2  # OPT_REDUNDANCY values
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
 ERR_OP = 9  # MPI_ERR_OP: a logical / bitwise op on a float type
 
@@ -46,7 +49,8 @@ class Stats(ctypes.Structure):
                 ("drain_s", ctypes.c_double), ("syncs", ctypes.c_int), ("relayed_steps", ctypes.c_int),
                 ("mesh_steps", ctypes.c_int), ("export_retries", ctypes.c_int),
                 ("gated_launches", ctypes.c_int), ("gated_skips", ctypes.c_int),
-                ("user_stream_waits", ctypes.c_int)]
+                ("user_stream_waits", ctypes.c_int), ("step0_copy", ctypes.c_int), ("gate_holds", ctypes.c_int),
+                ("gate_relaunches", ctypes.c_int)]
 
 
 class Kill(ctypes.Structure):

@@ -187,7 +187,7 @@ def plot_outcomes(c: dict, path: str, title: str = "single-kill outcomes") -> No
 def sweep_table(bench_json: str) -> pd.DataFrame:
     with open(bench_json) as f:
         d = json.loads([l for l in f.read().splitlines() if l.startswith("{")][-1])
-    rows = list(d.get("size_sweep_us", {}).values())
+    rows = [v for v in d.get("size_sweep_us", {}).values() if isinstance(v, dict)]  # (skip the setting keys)
     t = pd.DataFrame(rows).sort_values("bytes").reset_index(drop=True)
     t.attrs["n_gpus"] = d.get("n_gpus")
     return t

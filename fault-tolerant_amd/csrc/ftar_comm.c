@@ -154,11 +154,13 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->loop_seconds = getenv("FTAR_LOOP_SECONDS") ? atof(getenv("FTAR_LOOP_SECONDS")) : 0.0;
     c->overlap = getenv("FTAR_OVERLAP") ? atoi(getenv("FTAR_OVERLAP")) : 1;
     c->relay = getenv("FTAR_RELAY") ? atoi(getenv("FTAR_RELAY")) : 1;
-    c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 0;
+    c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 2;
+    if (c->redundancy < 0 || c->redundancy > 2) c->redundancy = 2;
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
     c->push = getenv("FTAR_PUSH") ? atoi(getenv("FTAR_PUSH")) : 0;
     c->gate = getenv("FTAR_GATE") ? atoi(getenv("FTAR_GATE")) != 0 : 1;
+    c->gate_hold_s = (getenv("FTAR_GATE_HOLD_US") ? atof(getenv("FTAR_GATE_HOLD_US")) : 2000.0) * 1e-6;
     c->oneshot_max = getenv("FTAR_ONESHOT_MAX") ? (size_t)atoll(getenv("FTAR_ONESHOT_MAX")) : ((size_t)1 << 20);
     c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
     c->stage_max = getenv("FTAR_STAGE_MAX") ? (size_t)atoll(getenv("FTAR_STAGE_MAX")) : ((size_t)1 << 20);
@@ -432,11 +434,20 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_RELAY_MIN: c->relay_min = (size_t)v; break;
     case FTAR_OPT_LOOP_SECONDS: c->loop_seconds = v; break;
     case FTAR_OPT_COPY_ENGINE: c->copy_engine = v != 0; break;
-    case FTAR_OPT_REDUNDANCY: c->redundancy = v != 0; break;
+    case FTAR_OPT_REDUNDANCY:
+        if (v != 0 && v != 1 && v != 2) return FTAR_ERR_ARG;
+        c->redundancy = (int)v;
+        break;
     case FTAR_OPT_MESH: c->mesh = v != 0; break;
     case FTAR_OPT_ONESHOT_MAX: c->oneshot_max = (size_t)v; break;
     case FTAR_OPT_PUSH: c->push = v >= 2 ? 2 : v != 0; break;
     case FTAR_OPT_GATE: c->gate = v != 0; break;
+    case FTAR_OPT_FLAG_SYNC:
+        if (fdev_set_knob(c->dev, FDEV_KNOB_FLAG_SYNC, v != 0)) return FTAR_ERR_ARG;
+        break;
+    case FTAR_OPT_TREE_UNROLL:
+        if (v != (int)v || fdev_set_knob(c->dev, FDEV_KNOB_TREE_UNROLL, (int)v)) return FTAR_ERR_ARG;
+        break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;
@@ -456,6 +467,8 @@ int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
     case FTAR_OPT_ONESHOT_MAX: *v = (double)c->oneshot_max; break;
     case FTAR_OPT_PUSH: *v = c->push; break;
     case FTAR_OPT_GATE: *v = c->gate; break;
+    case FTAR_OPT_FLAG_SYNC: *v = fdev_get_knob(c->dev, FDEV_KNOB_FLAG_SYNC); break;
+    case FTAR_OPT_TREE_UNROLL: *v = fdev_get_knob(c->dev, FDEV_KNOB_TREE_UNROLL); break;
     default: return FTAR_ERR_ARG;
     }
     return FTAR_SUCCESS;
@@ -501,13 +514,36 @@ uint64_t ftar_step_sync(ftar_comm *c, int nsteps)
     return ftar_sync(c);
 }
 
+/* A launch queued behind a gate spins at the head of this rank's stream -- and of any
+ * other stream of the process sharing its hardware queue -- until the barrier after which
+ * the host opens it.  When that barrier waits long (a late peer), the launch is given up
+ * (skip: its workgroups return untouched) and the step launches after the barrier instead:
+ * the stall stays bounded by FTAR_GATE_HOLD_US, and the device's own gate timeout is never
+ * reached while this process runs. */
+static void gate_hold(void *arg)
+{
+    ftar_comm *c = (ftar_comm *)arg;
+    if (!fdev_gate_pending(c->dev)) return;
+    fdev_gate_open(c->dev, 1);
+    c->stats.gate_holds++;
+    if (c->verbose)
+        fprintf(stderr, "ftar: rank %d: barrier waited past %.0f us: gated launch given up\n", c->wrank,
+                c->gate_hold_s * 1e6);
+}
+
 uint64_t ftar_sync(ftar_comm *c)
 {
     double t0 = now_s();
     uint64_t next = c->job.seq + 1;
     atomic_store_explicit(&c->job.shm->slot[c->wrank].pubv[next % 2], (next << 16) | ((uint64_t)c->pubval & 0xffff),
                           memory_order_release);
+    if (c->gate_hold_s > 0 && fdev_gate_pending(c->dev)) {
+        c->job.wait_hook = gate_hold;
+        c->job.wait_arg = c;
+        c->job.wait_after_s = c->gate_hold_s;
+    }
     uint64_t snap = ftar_ctrl_agree(&c->job, c->members);
+    c->job.wait_hook = NULL;
     double dt = now_s() - t0;
     c->stats.sync_wait_s += dt;
     c->stats.syncs++;
@@ -538,6 +574,13 @@ int64_t ftar_peer_pub(ftar_comm *c, int w)
 }
 
 int ftar_is_dead(ftar_comm *c, int w) { return ftar_ctrl_is_dead(&c->job, w); }
+
+int ftar_spans_devices(const ftar_comm *c)
+{
+    for (int i = 0; i < c->size; i++)
+        if (c->job.shm->slot[c->order[i]].device != c->job.shm->slot[c->order[0]].device) return 1;
+    return 0;
+}
 void ftar_enter(ftar_comm *c) { ftar_ctrl_enter(&c->job); }
 int ftar_peer_entered(ftar_comm *c, int w) { return ftar_ctrl_peer_entered(&c->job, w); }
 int ftar_peer_done(ftar_comm *c, int w) { return ftar_ctrl_peer_done(&c->job, w); }
@@ -848,6 +891,7 @@ void ftar_stats_end(ftar_comm *c)
     c->stats.comm_size_after = c->size;
     c->stats.export_retries = fdev_export_retries(c->dev);
     c->stats.user_stream_waits = fdev_user_host_waits(c->dev);
+    c->stats.gate_relaunches = fdev_gate_relaunches(c->dev);
     ftar_inputs_done(c);
 }
 

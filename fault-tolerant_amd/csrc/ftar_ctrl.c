@@ -259,6 +259,11 @@ uint64_t ftar_ctrl_agree(ftar_job *job, uint64_t members)
             }
             continue;
         }
+        if (job->wait_hook && (it & 255) == 255 && now_s() - t0 > job->wait_after_s) {
+            void (*h)(void *) = job->wait_hook;
+            job->wait_hook = NULL; /* once per round */
+            h(job->wait_arg);
+        }
         cpu_relax();
     }
 }

@@ -99,6 +99,11 @@ typedef struct {
     uint64_t seq; /* agree sequence number */
     uint64_t xtok; /* exchange token of the step this rank last entered (seq + 1 at entry) */
     int owner;    /* created the segment */
+    /* optional: called once by ftar_ctrl_agree when a round has waited longer than
+     * wait_after_s (the library gives up a launch queued behind a gate there) */
+    void (*wait_hook)(void *);
+    void *wait_arg;
+    double wait_after_s;
 } ftar_job;
 
 /* Create (launcher / rank 0) or attach (others) the segment named `name`. */

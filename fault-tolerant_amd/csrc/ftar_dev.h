@@ -39,6 +39,8 @@ typedef struct {
     const void *y;
     size_t n;         /* elements */
     void *out2;       /* optional second destination receiving the same values (local) */
+    int out2_pre;     /* FDEV_REDUCE only: out2 receives x as it was read (the pre-image of an in-place
+                         reduce), not the result */
 } fdev_seg;
 
 #define FDEV_MAX_SEGS 16 /* a relayed exchange step: 2 own pulls + 2 x 6 relay duties */
@@ -127,10 +129,19 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
 /* Open the pending gate (no-op without one).  skip = 1: the gated launch does nothing.
  * Any other launch or stream wait queued while a gate is pending opens it as skip first
  * (nothing may wait behind a closed gate): a caller about to open its gate checks
- * fdev_gate_pending and relaunches if the gated launch was given up. */
+ * fdev_gate_pending and relaunches if the gated launch was given up.
+ * A gate the DEVICE gave up on (still closed after FTAR_GATE_TIMEOUT_MS of its wall clock:
+ * the workgroups returned without touching memory) is caught by the next fdev_sync, which
+ * relaunches the same plan ungated and drains it (fdev_gate_relaunches counts them). */
 int fdev_gate_open(ftar_dev *d, int skip);
 /* 1 while a gated launch waits for its gate. */
 int fdev_gate_pending(const ftar_dev *d);
+int fdev_gate_relaunches(const ftar_dev *d);
+/* Per-rank knobs of the device layer (not collective). */
+#define FDEV_KNOB_FLAG_SYNC 0   /* 0/1: short launches signal their completion (off: fenced markers, no gates) */
+#define FDEV_KNOB_TREE_UNROLL 1 /* 1, 2, 4: vectors per lane and source in fdev_tree at 4 / 8 sources */
+int fdev_set_knob(ftar_dev *d, int knob, int value);
+int fdev_get_knob(const ftar_dev *d, int knob);
 /* Enqueue on the rank's background stream, ordered after everything queued so far on
  * the main stream (it then overlaps later main-stream work). */
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag);

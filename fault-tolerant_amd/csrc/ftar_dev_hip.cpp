@@ -134,12 +134,25 @@ struct ftar_dev {
     // that timed out (or was found overtaken) is reported in sig_flag[32].
     unsigned gate_seq;     // sequence of the last gate (the word's value = 2 x seq, + 1 = skip)
     int gate_pending;      // queued, gate still closed
-    int gate_verify;       // opened: check the timeout word at the next drain
+    int gate_verify;       // opened: check gate verify_seq's timeout word at the next drain
+    unsigned verify_seq;
     int pre_gate_any;      // signalled launches queued before the gated one since the last drain ...
     unsigned pre_gate_tag; // ... the last of them
     unsigned long long gate_ticks; // wall-clock ticks before a closed gate counts as timed out
     double gate_link, gate_hbm;    // the gated launch's bytes (counted if it runs)
     int user_host_waits;           // calls that found the caller's stream busy and waited for it
+    // The plan of each recent gated launch (by gate sequence parity: the one being verified
+    // and the one pending), kept so that a launch whose gate timed out on the device -- its
+    // workgroups returned without touching memory -- is relaunched ungated at the drain
+    // (gated launches never write what they read, so running a part of one twice is harmless).
+    struct GatedPlan {
+        int valid, batch, dtype, op, nsrc;
+        unsigned grid, seq;
+        ftar::KSegList L;
+        ftar::TreeBatch B;
+    } gp[2];
+    int gate_relaunches;
+    unsigned tree_unroll;          // FDEV_KNOB_TREE_UNROLL
 };
 
 extern "C" {
@@ -188,14 +201,28 @@ int fdev_open(int device, ftar_dev **out)
         d->unsignalled = d->signalled = d->need_acquire = d->force_fence = 0;
         d->gate_seq = 0;
         d->gate_pending = d->gate_verify = d->pre_gate_any = 0;
+        d->verify_seq = 0;
         d->user_host_waits = 0;
         d->pre_gate_tag = 0;
+        d->gate_relaunches = 0;
+        d->gp[0].valid = d->gp[1].valid = 0;
+        {
+            const char *tu = getenv("FTAR_TREE_UNROLL");
+            int u = tu ? atoi(tu) : 1;
+            d->tree_unroll = (u == 2 || u == 4) ? (unsigned)u : 1u;
+        }
         int khz = 0; // wall clock of the kernels (s_memrealtime), 100 MHz on CDNA
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
             (void)hipGetLastError();
             khz = 100000;
         }
-        d->gate_ticks = (unsigned long long)khz * 1000ull * 60ull; // 60 s
+        // FTAR_GATE_TIMEOUT_MS (default 60 s): a gate still closed this long is given up by
+        // the device (the workgroups return untouched) and the launch is relaunched ungated at
+        // the next drain; the host normally gives a gate up far sooner (FTAR_GATE_HOLD_US)
+        const char *gt = getenv("FTAR_GATE_TIMEOUT_MS");
+        long long ms = gt ? atoll(gt) : 60000;
+        if (ms < 1) ms = 1;
+        d->gate_ticks = (unsigned long long)khz * (unsigned long long)ms;
         if (d->flag_sync) {
             HIPCHK(hipMalloc((void **)&d->sig_cnt, 256));
             HIPCHK(hipMemset(d->sig_cnt, 0, 256));
@@ -209,7 +236,7 @@ int fdev_open(int device, ftar_dev **out)
                 d->sig_cnt = nullptr;
                 d->flag_sync = 0;
             } else {
-                memset(d->sig_flag, 0, 256); // flag [0], gate [16], gate timeout [32]
+                memset(d->sig_flag, 0, 256); // flag [0], gates [16..23], their timeout words [32..39]
                 __atomic_store_n(d->sig_flag, 0u, __ATOMIC_RELEASE);
             }
             HIPCHK(hipDeviceSynchronize());
@@ -457,6 +484,34 @@ static void note_launch(ftar_dev *d, hipStream_t st, unsigned grid, bool can_sig
     }
 }
 
+// The kernel's view of fdev segments, and their algorithmic link / HBM bytes.
+static void seg_inputs(const fdev_seg *segs, int nseg, size_t es, ftar::SegIn *in, double *link, double *hbm)
+{
+    for (int i = 0; i < nseg; i++) {
+        in[i].kind = segs[i].kind == FDEV_COPY ? ftar::kCopy : ftar::kReduce;
+        in[i].out = segs[i].out;
+        in[i].x = segs[i].x;
+        in[i].y = segs[i].y;
+        in[i].n = segs[i].n;
+        in[i].out2 = segs[i].out2;
+        in[i].out2_pre = segs[i].out2_pre;
+        double b = (double)segs[i].n * (double)es;
+        int nread = segs[i].kind == FDEV_COPY ? 1 : 2;
+        int nremote = ((segs[i].remote & FDEV_REMOTE_X) ? 1 : 0) +
+                      ((segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) ? 1 : 0);
+        int rout = (segs[i].remote & FDEV_REMOTE_OUT) ? 1 : 0;
+        *link += b * (nremote + rout);
+        *hbm += b * (1 - rout + nread - nremote + (segs[i].out2 ? 1 : 0));
+    }
+}
+
+// [a, a + na) and [b, b + nb) overlap
+static bool overlaps(const void *a, size_t na, const void *b, size_t nb)
+{
+    const char *x = (const char *)a, *y = (const char *)b;
+    return a && b && x < y + nb && y < x + na;
+}
+
 static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     size_t es = esize_of(dtype);
@@ -465,21 +520,10 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
         return 13;
     }
     ftar::SegIn in[FDEV_MAX_SEGS];
-    for (int i = 0; i < nseg; i++) {
-        in[i].kind = segs[i].kind == FDEV_COPY ? ftar::kCopy : ftar::kReduce;
-        in[i].out = segs[i].out;
-        in[i].x = segs[i].x;
-        in[i].y = segs[i].y;
-        in[i].n = segs[i].n;
-        in[i].out2 = segs[i].out2;
-        double b = (double)segs[i].n * (double)es;
-        int nread = segs[i].kind == FDEV_COPY ? 1 : 2;
-        int nremote = ((segs[i].remote & FDEV_REMOTE_X) ? 1 : 0) +
-                      ((segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) ? 1 : 0);
-        int rout = (segs[i].remote & FDEV_REMOTE_OUT) ? 1 : 0;
-        d->ctr.link_bytes += b * (nremote + rout);
-        d->ctr.hbm_bytes += b * (1 - rout + nread - nremote + (segs[i].out2 ? 1 : 0));
-    }
+    double link = 0, hbm = 0;
+    seg_inputs(segs, nseg, es, in, &link, &hbm);
+    d->ctr.link_bytes += link;
+    d->ctr.hbm_bytes += hbm;
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
     if (grid == 0) return 0;
@@ -527,7 +571,8 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
     }
     note_launch(d, d->stream, ~0u, false, nullptr);
     // pieces of at most max_blocks vector workgroups (plan_tree refuses larger bodies)
-    const size_t piece = (size_t)d->max_blocks * 256 * (16 / es);
+    const unsigned u = (nsrc == 4 || nsrc == 8) ? d->tree_unroll : 1u;
+    const size_t piece = (size_t)d->max_blocks * 256 * u * (16 / es);
     for (size_t off = 0; off < n; off += piece) {
         ftar::TreeArgs A;
         memset(&A, 0, sizeof(A));
@@ -537,6 +582,7 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
         for (int o = 0; o < nmore; o++) A.more[o] = (char *)more[o] + off * es;
         A.n = n - off < piece ? n - off : piece;
         A.nt_store = nt_store();
+        A.unroll = u;
         unsigned grid = ftar::plan_tree(&A, nsrc, es, d->max_blocks + 1);
         if (grid == 0) {
             snprintf(g_err, sizeof(g_err), "fdev_tree: plan failed");
@@ -552,8 +598,10 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
     return 0;
 }
 
-// Gate words: sig_flag[16 .. 23], gate `seq` in slot seq % kGateSlots.
+// Gate words: sig_flag[16 .. 23], gate `seq` in slot seq % kGateSlots; the slot's timeout
+// word sig_flag[32 + slot] (a workgroup that gave the gate up writes the gate's value).
 static unsigned *gate_word(ftar_dev *d, unsigned seq) { return d->sig_flag + 16 + seq % ftar::kGateSlots; }
+static unsigned *gate_err(ftar_dev *d, unsigned seq) { return d->sig_flag + 32 + seq % ftar::kGateSlots; }
 
 // Whether a launch of `grid` workgroups may be queued behind a gate now (see
 // fdev_tree_batch_gated): a fenced marker or an unsignalled launch would have to drain
@@ -573,10 +621,33 @@ static ftar::KSignal arm_gate(ftar_dev *d, double link, double hbm)
     d->pre_gate_tag = d->sig_tag;
     d->gate_seq++;
     d->signalled++;
+    __atomic_store_n(gate_err(d, d->gate_seq), 0u, __ATOMIC_RELAXED); // the slot's last gate was verified
     // the workgroups invalidate their caches once the gate opens (acquire = 1): whatever
     // the drains before it did, the peers' data is read fresh
     return ftar::KSignal{d->sig_cnt, d->sig_flag, ++d->sig_tag, 1u, gate_word(d, d->gate_seq), 2u * d->gate_seq,
-                         d->sig_flag + 32, d->gate_ticks};
+                         gate_err(d, d->gate_seq), d->gate_ticks};
+}
+
+// Keep the plan of the gate just armed (d->gate_seq) for a relaunch: the same launch with
+// no signal, gate or staging phase.
+static void keep_plan(ftar_dev *d, int batch, int dtype, int op, int nsrc, unsigned grid, const ftar::KSegList *L,
+                      const ftar::TreeBatch *B)
+{
+    ftar_dev::GatedPlan &g = d->gp[d->gate_seq & 1];
+    g.valid = 1;
+    g.batch = batch;
+    g.dtype = dtype;
+    g.op = op;
+    g.nsrc = nsrc;
+    g.grid = grid;
+    g.seq = d->gate_seq;
+    if (batch) {
+        g.B = *B;
+        g.B.sig = ftar::KSignal{nullptr, nullptr, 0, 0};
+    } else {
+        g.L = *L;
+        g.L.sig = ftar::KSignal{nullptr, nullptr, 0, 0};
+    }
 }
 
 // The TreeBatch of fdev_tree_batch(_gated): the grid (0 = a tree beyond the workgroup
@@ -620,12 +691,20 @@ int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *con
     double link, hbm;
     int rc = build_batch(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, &B, &grid, &link, &hbm);
     if (rc || !can_gate(d, grid)) return rc;
+    // only a launch that never writes what it reads is gated: a gate the device gave up on
+    // is relaunched whole, and some workgroups may have run already
+    const size_t es = esize_of(dtype);
+    for (int t = 0; t < B.nt; t++)
+        for (int k = 0; k < B.nt; k++)
+            for (int j = 0; j < nsrc; j++)
+                if (overlaps(B.t[t].out, B.t[t].n * es, B.t[k].src[j], B.t[k].n * es)) return 0;
     unsigned stage_tag = 0;
     if (stage_dst && stage_n) {
         stage_tag = ++d->sig_tag; // the launch raises the flag twice: staged, then done
-        d->ctr.hbm_bytes += 2.0 * (double)stage_n * (double)esize_of(dtype);
+        d->ctr.hbm_bytes += 2.0 * (double)stage_n * (double)es;
     }
     B.sig = arm_gate(d, link, hbm);
+    keep_plan(d, 1, dtype, op, nsrc, grid, nullptr, &B);
     if (stage_tag) {
         B.sig.stage_src = stage_src;
         B.sig.stage_dst = stage_dst;
@@ -661,10 +740,38 @@ int fdev_gate_open(ftar_dev *d, int skip)
     }
     d->gate_pending = 0;
     d->gate_verify = 1;
+    d->verify_seq = d->gate_seq;
     return 0;
 }
 
 int fdev_gate_pending(const ftar_dev *d) { return d->gate_pending; }
+
+int fdev_gate_relaunches(const ftar_dev *d) { return d->gate_relaunches; }
+
+int fdev_set_knob(ftar_dev *d, int knob, int value)
+{
+    switch (knob) {
+    case FDEV_KNOB_FLAG_SYNC:
+        if (value && !d->sig_flag) return 13; // the pinned words were never set up (FTAR_FLAG_SYNC=0 at open)
+        if (d->gate_pending) (void)fdev_gate_open(d, 1);
+        d->flag_sync = value != 0;
+        return 0;
+    case FDEV_KNOB_TREE_UNROLL:
+        if (value != 1 && value != 2 && value != 4) return 13;
+        d->tree_unroll = (unsigned)value;
+        return 0;
+    default: return 13;
+    }
+}
+
+int fdev_get_knob(const ftar_dev *d, int knob)
+{
+    switch (knob) {
+    case FDEV_KNOB_FLAG_SYNC: return d->flag_sync;
+    case FDEV_KNOB_TREE_UNROLL: return (int)d->tree_unroll;
+    default: return -1;
+    }
+}
 
 int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, const unsigned *remote_mask,
                     void *const *out, const size_t *n, int ntree, int tag)
@@ -715,21 +822,15 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
     }
     ftar::SegIn in[FDEV_MAX_SEGS];
     double link = 0, hbm = 0;
-    for (int i = 0; i < nseg; i++) {
-        in[i].kind = segs[i].kind == FDEV_COPY ? ftar::kCopy : ftar::kReduce;
-        in[i].out = segs[i].out;
-        in[i].x = segs[i].x;
-        in[i].y = segs[i].y;
-        in[i].n = segs[i].n;
-        in[i].out2 = segs[i].out2;
-        double b = (double)segs[i].n * (double)es;
-        int nread = segs[i].kind == FDEV_COPY ? 1 : 2;
-        int nremote = ((segs[i].remote & FDEV_REMOTE_X) ? 1 : 0) +
-                      ((segs[i].kind != FDEV_COPY && (segs[i].remote & FDEV_REMOTE_Y)) ? 1 : 0);
-        int rout = (segs[i].remote & FDEV_REMOTE_OUT) ? 1 : 0;
-        link += b * (nremote + rout);
-        hbm += b * (1 - rout + nread - nremote + (segs[i].out2 ? 1 : 0));
-    }
+    seg_inputs(segs, nseg, es, in, &link, &hbm);
+    // only a launch that never writes what it reads is gated (see fdev_tree_batch_staged_gated)
+    for (int i = 0; i < nseg; i++)
+        for (int k = 0; k < nseg; k++) {
+            const size_t ni = segs[i].n * es, nk = segs[k].n * es;
+            for (void *o : {segs[i].out, segs[i].out2})
+                if (overlaps(o, ni, segs[k].x, nk) || (segs[k].kind != FDEV_COPY && overlaps(o, ni, segs[k].y, nk)))
+                    return 0;
+        }
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
     if (!can_gate(d, grid)) return 0;
@@ -740,6 +841,7 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
         d->ctr.hbm_bytes += 2.0 * (double)stage_n * (double)es;
     }
     L.sig = arm_gate(d, link, hbm);
+    keep_plan(d, 0, dtype, op, 0, grid, &L, nullptr);
     if (stage_tag) {
         L.sig.stage_src = stage_src;
         L.sig.stage_dst = stage_dst;
@@ -875,6 +977,41 @@ static int wait_signal(ftar_dev *d, unsigned tag, int (*poll)(void *), void *arg
     }
 }
 
+// The opened gate d->verify_seq has completed: did the device give it up (its gate stayed
+// closed past the timeout, or a late workgroup found the slot overtaken)?  Then its
+// workgroups (some or all) returned without touching memory, and the plan runs again
+// ungated -- after a fenced marker (device-wide acquire: the peers' current data) and
+// drained through one (release: visible to the peers before this rank arrives anywhere).
+// Any launch pending behind its own gate is given up first (nothing waits behind a closed
+// gate); its step then launches normally.
+static int verify_gate(ftar_dev *d, int (*poll)(void *), void *arg)
+{
+    if (!d->gate_verify) return 0;
+    d->gate_verify = 0;
+    const unsigned seq = d->verify_seq;
+    unsigned *err = gate_err(d, seq);
+    if (__atomic_load_n(err, __ATOMIC_ACQUIRE) != 2u * seq) return 0;
+    __atomic_store_n(err, 0u, __ATOMIC_RELAXED);
+    ftar_dev::GatedPlan &g = d->gp[seq & 1];
+    if (!g.valid || g.seq != seq) {
+        snprintf(g_err, sizeof(g_err), "gated launch %u: its gate timed out and its plan is gone", seq);
+        return 101;
+    }
+    if (d->gate_pending) (void)fdev_gate_open(d, 1);
+    fprintf(stderr, "ftar: device %d: gated launch %u was given up by the device (gate timeout): relaunched\n",
+            d->device, seq);
+    HIPCHK(hipEventRecord(d->fence_main, d->stream));
+    hipError_t e = g.batch ? ftar::launch_tree_batch(g.dtype, g.op, g.nsrc, g.B, g.grid, d->stream)
+                           : ftar::launch_segments(g.dtype, g.op, g.L, g.grid, d->stream);
+    if (e != hipSuccess) return set_err(e, "relaunch of a timed-out gated launch");
+    g.valid = 0;
+    d->gate_relaunches++;
+    int rc = sync_stream(d, d->stream, poll, arg);
+    d->need_acquire = 0;
+    d->unsignalled = d->signalled = d->force_fence = 0;
+    return rc;
+}
+
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 {
     int rc;
@@ -887,6 +1024,10 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
         d->pre_gate_any = 0;
         d->unsignalled = d->force_fence = 0;
         d->signalled = 1; // the gated launch, drained after its gate opens
+        if (rc) return rc;
+        // an earlier gated launch among them (RD: step s, opened; step s + 1 pending) has
+        // completed too: check it now, before step s + 1 can read its result
+        rc = verify_gate(d, poll, arg);
         if (rc) return rc;
         return harvest(d);
     }
@@ -903,16 +1044,8 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
     }
     d->unsignalled = d->signalled = d->force_fence = 0;
     if (rc) return rc;
-    if (d->gate_verify) { // the gated launch has completed: did its gate time out?
-        d->gate_verify = 0;
-        unsigned t = __atomic_load_n(d->sig_flag + 32, __ATOMIC_ACQUIRE);
-        if (t) {
-            __atomic_store_n(d->sig_flag + 32, 0u, __ATOMIC_RELAXED);
-            snprintf(g_err, sizeof(g_err), "gated launch %u: its gate stayed closed past the timeout (or was overtaken)",
-                     t / 2);
-            return 101;
-        }
-    }
+    rc = verify_gate(d, poll, arg); // the gated launch has completed: did its gate time out?
+    if (rc) return rc;
     return harvest(d);
 }
 

@@ -82,10 +82,12 @@ struct ftar_comm {
     int relay;           /* FTAR_RELAY (default 1): stripe exchanges over 2-hop paths */
     size_t relay_min;    /* FTAR_RELAY_MIN bytes: smallest per-rank window that is relayed */
     int copy_engine;     /* FTAR_COPY_ENGINE (default 0): direct pulls by hipMemcpyAsync */
-    int redundancy;      /* FTAR_REDUNDANCY (default 0: the step-0 copy is never moved; a replay reads the dead rank's IN) */
+    int redundancy;      /* FTAR_REDUNDANCY: 2 auto (default: the step-0 copy moves where a spare exists and the
+                            comm spans GPUs), 1 always, 0 never (a replay reads the dead rank's IN) */
     int mesh;            /* FTAR_MESH (default 1): one-hop Raben at power-of-two p without a spare */
     int push;            /* FTAR_PUSH (default 0): the mesh by remote stores -- 1 reduce-scatter, 2 both phases */
     int gate;            /* FTAR_GATE (default 1): small exchange launches queued ahead of their barrier, gated */
+    double gate_hold_s;  /* FTAR_GATE_HOLD_US: a barrier waiting longer gives the pending gated launch up (0 = never) */
     size_t oneshot_max;  /* FTAR_ONESHOT_MAX bytes: mesh Raben in one launch up to this size */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
     /* the step's last peer read (FTAR_LOOP_SECONDS re-pulls it into pad while it waits) */
@@ -158,6 +160,8 @@ void ftar_note_launch(ftar_comm *c, const void *remote, size_t bytes);
 int ftar_run_bg(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);
 int ftar_drain_bg(ftar_comm *c);
 int ftar_is_dead(ftar_comm *c, int w);
+/* 1 if the comm's members drive more than one GPU (uniform: the same on every member) */
+int ftar_spans_devices(const ftar_comm *c);
 /* Exchange entry (see ftar_ctrl_enter): a partner's exchange failed iff it died before
  * entering it -- what the reference's failed Sendrecv means -- independent of when the
  * death is noticed (a rank that dies after its exchange point is still read). */
@@ -197,6 +201,7 @@ typedef struct {
     int dst_buf, x_buf;
     int64_t off, n;
     int to_uout; /* also store the result in the caller's output buffer (same offset) */
+    int save_pre; /* REDUCE: the same launch stores the local operand's pre-image into T (same offset) */
 } ftar_pull;
 
 #define FTAR_MAX_PULLS 2

@@ -40,7 +40,7 @@ struct KSignal {
     unsigned acquire;
     const unsigned *gate; // pinned host word (slot gate_val / 2 % kGateSlots); nullptr = not gated
     unsigned gate_val;
-    unsigned *err;        // pinned host word: set to gate_val on a gate timeout
+    unsigned *err;        // pinned host word of this gate's slot: set to gate_val on a gate timeout
     unsigned long long gate_ticks;
     // Optional staging phase BEFORE the gate (a gated launch that also stages this rank's
     // input for its peers, saving the separate staging launch): every workgroup copies its
@@ -63,6 +63,7 @@ struct KSeg {
     size_t n;
     unsigned kind;
     unsigned vec;
+    unsigned pre2;       // reduce: out2 receives x as read (the pre-image), not the result
     unsigned blk_begin;  // sequential region: blocks [blk_begin, blk_end) ...
     unsigned blk_end;
     unsigned tile_base;  // ... take tiles tile_base, tile_base + 1, ... of this piece
@@ -119,6 +120,7 @@ struct SegIn {
     const void *y;
     size_t n;
     void *out2;
+    int out2_pre; // reduce: out2 receives x (pre-image)
 };
 
 // Tree reduce: out[i] = balanced left-to-right tree of src[0..p-1][i] (p = 2, 4, 8, 16):
@@ -137,8 +139,10 @@ struct TreeArgs {
     size_t nv;     // 16-byte vectors in the body (0 when the pointers are not co-aligned)
     unsigned nvb;  // workgroups of the vector body; the rest do the scalar elements
     unsigned nt_store; // 16-byte stores non-temporal
+    unsigned unroll;   // 16-byte vectors per lane and source (1, 2, 4; > 1 only for tree_kernel at p = 4, 8)
 };
-// fills the alignment fields of A (src/out/n set) and returns the grid size
+constexpr int kMaxUnroll = 4;
+// fills the alignment fields of A (src/out/n/unroll set) and returns the grid size
 unsigned plan_tree(TreeArgs *A, int p, size_t esize, unsigned max_blocks);
 hipError_t launch_tree(int dtype, int op, int p, const TreeArgs &A, unsigned grid, hipStream_t s);
 // up to kMaxBatch trees of p <= kMaxBatchP sources in one launch; tree k owns

@@ -235,6 +235,9 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk, u
     const uint4 *__restrict__ Y = (const uint4 *)S.y;
     uint4 *__restrict__ O = (uint4 *)S.out;
     uint4 *__restrict__ O2 = (uint4 *)S.out2; // wave-uniform: both stores or one
+    // pre2 (wave-uniform): O2 receives x as read -- the pre-image of an in-place reduce,
+    // saved by the same pass that overwrites it (the configs[4] mid-exchange guard)
+    const bool pre = S.pre2 != 0 && S.kind != kCopy;
     const size_t nv = S.n / E;
     for (size_t base = b * kTile; base < nv; base += nblk * kTile) {
         const size_t i = base + threadIdx.x;
@@ -245,20 +248,25 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk, u
             if (S.kind != kCopy) {
 #pragma unroll
                 for (int u = 0; u < kUnroll; u++) c[u] = ldnt(Y + i + u * kBlock);
+                if (pre) {
+#pragma unroll
+                    for (int u = 0; u < kUnroll; u++) st16(O2 + i + u * kBlock, a[u], nts);
+                }
 #pragma unroll
                 for (int u = 0; u < kUnroll; u++) a[u] = apply16<T, OP>(a[u], c[u]);
             }
 #pragma unroll
             for (int u = 0; u < kUnroll; u++) st16(O + i + u * kBlock, a[u], nts);
-            if (O2) {
+            if (O2 && !pre) {
 #pragma unroll
                 for (int u = 0; u < kUnroll; u++) st16(O2 + i + u * kBlock, a[u], nts);
             }
         } else {
             for (size_t j = i; j < nv; j += kBlock) {
-                const uint4 v = (S.kind == kCopy) ? ldnt(X + j) : apply16<T, OP>(ldnt(X + j), ldnt(Y + j));
+                const uint4 xv = ldnt(X + j);
+                const uint4 v = (S.kind == kCopy) ? xv : apply16<T, OP>(xv, ldnt(Y + j));
                 st16(O + j, v, nts);
-                if (O2) st16(O2 + j, v, nts);
+                if (O2) st16(O2 + j, pre ? xv : v, nts);
             }
         }
     }
@@ -271,11 +279,13 @@ __device__ __forceinline__ void scalar_body(const KSeg &S, size_t b, size_t nblk
     const T *Y = (const T *)S.y;
     T *O = (T *)S.out;
     T *O2 = (T *)S.out2;
+    const bool pre = S.pre2 != 0 && S.kind != kCopy;
     const size_t stride = nblk * kBlock;
     for (size_t i = b * kBlock + threadIdx.x; i < S.n; i += stride) {
-        const T v = (S.kind == kCopy) ? X[i] : apply<T, OP>(X[i], Y[i]);
+        const T xv = X[i];
+        const T v = (S.kind == kCopy) ? xv : apply<T, OP>(xv, Y[i]);
         O[i] = v;
-        if (O2) O2[i] = v;
+        if (O2) O2[i] = pre ? xv : v;
     }
 }
 
@@ -335,21 +345,45 @@ __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(uint4 *__restrict__ 
 // stream at once -- and combines them in the schedule's tree.  Workgroups past the
 // vector body take the scalar head/tail (or everything, if the pointers are not
 // co-aligned), grid-stride.
+// U (1, 2, 4): 16-byte vectors per lane and source, every load of the workgroup's U x P
+// vectors issued before the first combine -- more bytes in flight per lane when the
+// sources are remote (xGMI load latency) rather than local HBM (FTAR_OPT_TREE_UNROLL; the
+// node's transport selection times the forms).  Same tree per element: same bits.
 template <typename T, int OP, int P>
+__device__ __forceinline__ void tree_store(const TreeArgs &A, size_t i, uint4 (&v)[P])
+{
+#pragma unroll
+    for (int w = 1; w < P; w <<= 1)
+#pragma unroll
+        for (int j = 0; j < P; j += 2 * w) v[j] = apply16<T, OP>(v[j], v[j + w]);
+    st16((uint4 *)((T *)A.out + A.head) + i, v[0], A.nt_store);
+    for (int o = 0; o < A.nmore; o++) st16((uint4 *)((T *)A.more[o] + A.head) + i, v[0], A.nt_store);
+}
+
+template <typename T, int OP, int P, int U>
 __device__ __forceinline__ void tree_body(const TreeArgs &A, unsigned b, unsigned nblocks)
 {
     if (b < A.nvb) {
-        const size_t i = (size_t)b * kBlock + threadIdx.x;
-        if (i >= A.nv) return;
-        uint4 v[P];
+        const size_t i0 = (size_t)b * kBlock * U + threadIdx.x;
+        if (i0 + (size_t)(U - 1) * kBlock < A.nv) {
+            uint4 v[U][P];
 #pragma unroll
-        for (int j = 0; j < P; j++) v[j] = ldnt((const uint4 *)((const T *)A.src[j] + A.head) + i);
+            for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int w = 1; w < P; w <<= 1)
+                for (int j = 0; j < P; j++)
+                    v[u][j] = ldnt((const uint4 *)((const T *)A.src[j] + A.head) + i0 + (size_t)u * kBlock);
 #pragma unroll
-            for (int j = 0; j < P; j += 2 * w) v[j] = apply16<T, OP>(v[j], v[j + w]);
-        st16((uint4 *)((T *)A.out + A.head) + i, v[0], A.nt_store);
-        for (int o = 0; o < A.nmore; o++) st16((uint4 *)((T *)A.more[o] + A.head) + i, v[0], A.nt_store);
+            for (int u = 0; u < U; u++) tree_store<T, OP, P>(A, i0 + (size_t)u * kBlock, v[u]);
+        } else {
+            for (int u = 0; u < U; u++) {
+                const size_t i = i0 + (size_t)u * kBlock;
+                if (i >= A.nv) break;
+                uint4 v[P];
+#pragma unroll
+                for (int j = 0; j < P; j++) v[j] = ldnt((const uint4 *)((const T *)A.src[j] + A.head) + i);
+                tree_store<T, OP, P>(A, i, v);
+            }
+        }
         return;
     }
     constexpr size_t E = 16 / sizeof(T);
@@ -370,10 +404,10 @@ __device__ __forceinline__ void tree_body(const TreeArgs &A, unsigned b, unsigne
     }
 }
 
-template <typename T, int OP, int P>
+template <typename T, int OP, int P, int U>
 __global__ __launch_bounds__(kBlock) void tree_kernel(TreeArgs A)
 {
-    tree_body<T, OP, P>(A, (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x), gridDim.x);
+    tree_body<T, OP, P, U>(A, (unsigned)__builtin_amdgcn_readfirstlane((int)blockIdx.x), gridDim.x);
 }
 
 // Several trees in one launch (the one-shot mesh Allreduce: every block of the vector,
@@ -387,7 +421,7 @@ __global__ __launch_bounds__(kBlock) void tree_batch_kernel(TreeBatch B)
     signal_stage(B.sig);
     if (signal_gate(B.sig)) {
         signal_acquire(B.sig);
-        tree_body<T, OP, P>(B.t[k], b - B.first[k], B.first[k + 1] - B.first[k]);
+        tree_body<T, OP, P, 1>(B.t[k], b - B.first[k], B.first[k + 1] - B.first[k]);
     }
     signal_done(B.sig);
 }
@@ -409,7 +443,9 @@ unsigned plan_tree(TreeArgs *A, int p, size_t esize, unsigned max_blocks)
         A->nv = (A->n - head) * esize / 16;
     }
     size_t nscalar = A->n - A->nv * (16 / esize);
-    size_t vb = (A->nv + kBlock - 1) / kBlock;
+    const unsigned u = (A->unroll == 2 || A->unroll == 4) && (p == 4 || p == 8) ? A->unroll : 1;
+    A->unroll = u;
+    size_t vb = (A->nv + (size_t)kBlock * u - 1) / ((size_t)kBlock * u);
     if (vb > max_blocks) return 0; // the caller splits larger blocks
     size_t sb = (nscalar + kBlock - 1) / kBlock;
     if (sb > 256) sb = 256;
@@ -417,14 +453,30 @@ unsigned plan_tree(TreeArgs *A, int p, size_t esize, unsigned max_blocks)
     return (unsigned)(vb + sb);
 }
 
+template <typename T, int OP, int P>
+static void launch_tree_u(const TreeArgs &A, unsigned grid, hipStream_t s)
+{
+    if constexpr (P == 4 || P == 8) {
+        if (A.unroll == 4) {
+            hipLaunchKernelGGL((tree_kernel<T, OP, P, 4>), dim3(grid), dim3(kBlock), 0, s, A);
+            return;
+        }
+        if (A.unroll == 2) {
+            hipLaunchKernelGGL((tree_kernel<T, OP, P, 2>), dim3(grid), dim3(kBlock), 0, s, A);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((tree_kernel<T, OP, P, 1>), dim3(grid), dim3(kBlock), 0, s, A);
+}
+
 template <typename T, int OP>
 static hipError_t launch_tree_op(int p, const TreeArgs &A, unsigned grid, hipStream_t s)
 {
     switch (p) {
-    case 2: hipLaunchKernelGGL((tree_kernel<T, OP, 2>), dim3(grid), dim3(kBlock), 0, s, A); break;
-    case 4: hipLaunchKernelGGL((tree_kernel<T, OP, 4>), dim3(grid), dim3(kBlock), 0, s, A); break;
-    case 8: hipLaunchKernelGGL((tree_kernel<T, OP, 8>), dim3(grid), dim3(kBlock), 0, s, A); break;
-    case 16: hipLaunchKernelGGL((tree_kernel<T, OP, 16>), dim3(grid), dim3(kBlock), 0, s, A); break;
+    case 2: launch_tree_u<T, OP, 2>(A, grid, s); break;
+    case 4: launch_tree_u<T, OP, 4>(A, grid, s); break;
+    case 8: launch_tree_u<T, OP, 8>(A, grid, s); break;
+    case 16: launch_tree_u<T, OP, 16>(A, grid, s); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -451,6 +503,7 @@ unsigned plan_tree_batch(TreeBatch *B, int p, size_t esize, unsigned max_blocks)
     unsigned total = 0;
     for (int k = 0; k < B->nt; k++) {
         B->first[k] = total;
+        B->t[k].unroll = 1; // tree_batch_kernel is instantiated for one vector per lane and source
         unsigned g = plan_tree(&B->t[k], p, esize, max_blocks);
         if (g == 0) return 0;
         total += g;
@@ -570,6 +623,7 @@ unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_bloc
             k.n = n;
             k.kind = (unsigned)g.kind;
             k.vec = vec;
+            k.pre2 = (g.out2 && g.out2_pre && g.kind != kCopy) ? 1u : 0u;
             k.blk_begin = k.blk_end = 0;
             pieces[np].k = k;
             pieces[np].bytes = n * esize;

@@ -134,7 +134,10 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
             pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0], 0};
             P->npull[cr] = x->keep_recov ? 2 : 1;
         } else {
-            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_W, WS_W, WS_W, ri[step], rc[step], 0};
+            /* with an idle rank a partner's death mid-exchange is recoverable and the pulled
+             * window must then be discarded (corr, :238-241): the pull keeps its pre-image in
+             * T (see the reduce-scatter loop) */
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_W, WS_W, WS_W, ri[step], rc[step], 0, x->rem > 0};
             P->npull[cr] = 1;
         }
     }
@@ -652,14 +655,21 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * an RS error handler's replay, and every handler aborts before replaying when
      * there is no idle spare (new_entry = 2 rem - 1 = -1, errhandler.c:207-211,377-378).
      * rem only decreases during a call, so with rem = 0 at the start the copy can never
-     * be consumed: skip it (FTAR_REDUNDANCY=1 keeps it, the reference's shape). */
-    x->keep_recov = c->redundancy;
+     * be consumed: skip it (FTAR_REDUNDANCY=1 keeps it, the reference's shape).
+     * With a spare, the copy is what lets the replay survive the loss of the dead rank's
+     * memory (the reference copies at step 0 precisely because that memory is gone,
+     * :206-211).  A peer's mapping keeps a killed process's memory readable on one device
+     * (tested), but across GPUs that premise is unverified, so by default (auto, 2) the
+     * copy moves whenever the comm spans more than one GPU; FTAR_REDUNDANCY=0 elides it on
+     * any layout (the replay then reads the dead rank's input in place, deviation 6).
+     * Uniform: the members' devices are the same on every rank. */
+    x->keep_recov = c->redundancy == 1 || (c->redundancy == 2 && x->rem > 0 && ftar_spans_devices(c));
     /* The reference's recovery data: every rank holds its step-0 partner's other half (in
      * tmp) while a spare can use it, except a replacement rank (errhandler.c:213-241 ships
      * it the dead rank's state, not its redundancy: a replay by it aborts, as the oracle's
      * restatement does).  Without the physical copy (keep_recov = 0) the replay reads that
      * half where it lies: the IN of the rank that held the vrank at step 0. */
-    x->has_recov = c->redundancy || x->rem > 0;
+    x->has_recov = x->keep_recov || x->rem > 0;
     /* Without an idle rank every failure aborts (new_entry = -1, errhandler.c:207-211,
      * 377-378), so nothing outside the schedule has to stay recoverable: step 0 reads
      * this rank's reduce half straight from sbuf (only the half peers pull is staged in
@@ -679,6 +689,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);
+    c->stats.step0_copy = x->keep_recov && c->size > 1;
     if (c->size == 1) return ftar_single_rank(c, sbuf, rbuf, count * x->es);
 
     size_t bytes = count * x->es;
@@ -804,9 +815,12 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
          * and the RS handler rebuilds it from the impersonator's replay.  The pull reduces in
          * place, so while a recovery is possible (an idle rank exists; at step 0 the handler
          * aborts) the window's pre-image is kept in T -- whose half rw0 is unused (T holds
-         * the partner's other half, sw0) -- to undo the reduce. */
+         * the partner's other half, sw0) -- to undo the reduce.  The pull kernel stores it
+         * itself (rb_plan's save_pre: each stripe's local operand, as read, to T at the same
+         * offset), so the guard costs one extra 16-byte store per vector and no pass of its
+         * own.  If a relay died the window may be partly unreduced, but then a second rank
+         * died with the partner and the handler aborts (nf > 1, errhandler.c:37-38). */
         int guard = x->rem > 0 && step >= 1 && pw >= 0 && !skip;
-        if (guard) run_copy(x, at(x, T, x->rindex[step]), at(x, W, x->rindex[step]), x->rcount[step], 0, FDEV_TAG_LOCAL);
         double lb0 = ftar_link_bytes(c);
         int tag = step == 0 ? FDEV_TAG_STEP0 : FDEV_TAG_STEP;
         if (step == 0 && c->overlap && !ftar_xfer_would_relay(c, &P, x->es)) {
@@ -934,7 +948,7 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
     int p = c->size;
     int nchunk = 1;
     int commutes = dtype == FTAR_INT32 || dtype == FTAR_INT64 || op == FTAR_SUM || op == FTAR_PROD;
-    if (c->host_pipe && commutes && !c->redundancy && c->loop_seconds <= 0 && p >= 2 && (p & (p - 1)) == 0 &&
+    if (c->host_pipe && commutes && c->redundancy != 1 && c->loop_seconds <= 0 && p >= 2 && (p & (p - 1)) == 0 &&
         bytes >= HOST_PIPE_MIN) {
         nchunk = (int)(bytes / HOST_PIPE_CHUNK);
         if (nchunk > HOST_PIPE_MAX) nchunk = HOST_PIPE_MAX;

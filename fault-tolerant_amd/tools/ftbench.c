@@ -70,7 +70,7 @@ int main(int argc, char **argv)
     CHECK_HIP(hipDeviceSynchronize());
 
     double ms[MAX_CALLS], value[MAX_CALLS];
-    int rc[MAX_CALLS], rec[MAX_CALLS], size_after[MAX_CALLS], uniform[MAX_CALLS];
+    int rc[MAX_CALLS], rec[MAX_CALLS], size_after[MAX_CALLS], uniform[MAX_CALLS], step0_copy = 0;
     for (int c = 0; c < calls; c++) {
         rc[c] = rd ? ftar_recursive_doubling(s, r, count, FTAR_FLOAT32, FTAR_SUM, comm)
                    : ftar_allreduce_rabenseifner(s, r, count, FTAR_FLOAT32, FTAR_SUM, comm);
@@ -79,6 +79,7 @@ int main(int argc, char **argv)
         ms[c] = st.wall_s * 1e3;
         rec[c] = st.recoveries;
         size_after[c] = st.comm_size_after;
+        step0_copy |= st.step0_copy;
         /* outside the call's timed region: read the result back and check it is uniform */
         CHECK_HIP(hipMemcpy(h, r, count * sizeof(float), hipMemcpyDeviceToHost));
         value[c] = h[0];
@@ -97,7 +98,8 @@ int main(int argc, char **argv)
             }
         }
     }
-    printf("{\"rank\": %d, \"size\": %d, \"device\": %d, \"calls\": [", wrank, wsize, dev);
+    printf("{\"rank\": %d, \"size\": %d, \"device\": %d, \"step0_copy\": %d, \"calls\": [", wrank, wsize, dev,
+           step0_copy);
     for (int c = 0; c < calls; c++)
         printf("%s{\"rc\": %d, \"ms\": %.4f, \"recoveries\": %d, \"comm_size\": %d, \"value\": %.1f, \"uniform\": %s}",
                c ? ", " : "", rc[c], ms[c], rec[c], size_after[c], value[c], uniform[c] ? "true" : "false");

@@ -194,7 +194,12 @@ typedef enum {
     FTAR_OPT_RELAY_MIN = 2,    /* smallest window, in bytes, that is relayed */
     FTAR_OPT_LOOP_SECONDS = 3, /* stretch of the step loop for fault-injection runs */
     FTAR_OPT_COPY_ENGINE = 4,  /* direct pulls as hipMemcpyAsync copies + local reduce (0/1) */
-    FTAR_OPT_REDUNDANCY = 5,   /* Raben step-0 recovery copy: 0 only when a spare exists, 1 always */
+    FTAR_OPT_REDUNDANCY = 5,   /* Raben step-0 recovery copy (the reference's tmp, raben/rabenseifner.c:
+                                  206-211): 2 = auto (default): moved when a spare exists and the comm
+                                  spans more than one GPU, else a replay reads the dead rank's input
+                                  in place; 1 = always moved (the reference's shape, also at
+                                  power-of-two p); 0 = never moved (opt-in: the replay reads the dead
+                                  rank's input through its peer mapping on any layout) */
     FTAR_OPT_MESH = 6,         /* Raben at power-of-two p without a spare: one-hop reduce-scatter and
                                   allgather over the full mesh, same reduction tree (0/1) */
     FTAR_OPT_ONESHOT_MAX = 7,  /* mesh Raben up to this many bytes per vector (any size at p = 2): one
@@ -203,10 +208,20 @@ typedef enum {
                                   of each block into the owner's HBM, the owner reduces locally), 2 = both
                                   phases (the owner's tree also stores its block into every peer; p <= 8),
                                   0 = remote loads (default) */
-    FTAR_OPT_GATE = 9          /* queue small exchange launches (Raben one-shot, RD steps) ahead of the
+    FTAR_OPT_GATE = 9,         /* queue small exchange launches (Raben one-shot, RD steps) ahead of the
                                   barrier that readies their operands, the staging copy folded into the
                                   first, their workgroups waiting on a gate the barrier opens (0/1,
-                                  default 1): the launch latency overlaps the wait for the peers */
+                                  default 1): the launch latency overlaps the wait for the peers.  A
+                                  barrier that waits longer than FTAR_GATE_HOLD_US (default 2000 us)
+                                  gives the gated launch up and the step launches after it; a gate the
+                                  device gave up on (FTAR_GATE_TIMEOUT_MS, default 60000) is relaunched
+                                  ungated at the next drain */
+    FTAR_OPT_FLAG_SYNC = 10,   /* short launches (<= 64 workgroups) signal their own completion through
+                                  a pinned host word instead of a fenced marker drain (0/1, default 1;
+                                  0 also turns the gates off) */
+    FTAR_OPT_TREE_UNROLL = 11  /* 16-byte vectors per lane and source in the mesh's tree kernel at
+                                  p = 4, 8 (1, 2 or 4; default 1): more loads in flight per lane for
+                                  remote (xGMI) sources; same bits */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);
@@ -236,6 +251,10 @@ typedef struct {
     int    gated_skips;      /* ... of them replaced after the barrier (a peer's input moved) */
     int    user_stream_waits; /* calls that found the caller's stream busy and waited for it on the host,
                                  cumulative since ftar_init */
+    int    step0_copy;       /* Raben: this call moved the step-0 recovery copy (FTAR_OPT_REDUNDANCY) */
+    int    gate_holds;       /* gated launches given up because their barrier waited past FTAR_GATE_HOLD_US */
+    int    gate_relaunches;  /* gated launches the device gave up on (gate timeout), relaunched ungated;
+                                cumulative since ftar_init */
 } ftar_stats;
 
 int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);

@@ -40,6 +40,7 @@ struct ftar_dev {
         fdev_seg segs[FDEV_MAX_SEGS];
     } gated;
     uint64_t gates_run, gates_skipped;
+    int flag_sync, tree_unroll; /* knobs: no flag path here; flag_sync = 0 turns the gates off, as on the GPU */
 };
 
 #define MAXMAP 256
@@ -66,9 +67,32 @@ int fdev_open(int device, ftar_dev **out)
 {
     ftar_dev *d = (ftar_dev *)calloc(1, sizeof(ftar_dev));
     d->device = device;
+    d->flag_sync = getenv("FTAR_FLAG_SYNC") ? atoi(getenv("FTAR_FLAG_SYNC")) != 0 : 1;
+    d->tree_unroll = 1;
     *out = d;
     return 0;
 }
+
+int fdev_set_knob(ftar_dev *d, int knob, int value)
+{
+    if (knob == FDEV_KNOB_FLAG_SYNC) {
+        if (d->gate_pending) fdev_gate_open(d, 1);
+        d->flag_sync = value != 0;
+        return 0;
+    }
+    if (knob == FDEV_KNOB_TREE_UNROLL && (value == 1 || value == 2 || value == 4)) {
+        d->tree_unroll = value; /* the loops here have no vectors: same result */
+        return 0;
+    }
+    return 13;
+}
+
+int fdev_get_knob(const ftar_dev *d, int knob)
+{
+    return knob == FDEV_KNOB_FLAG_SYNC ? d->flag_sync : knob == FDEV_KNOB_TREE_UNROLL ? d->tree_unroll : -1;
+}
+
+int fdev_gate_relaunches(const ftar_dev *d) { return 0; }
 
 void fdev_close(ftar_dev *d) { free(d); }
 int fdev_device(const ftar_dev *d) { return d->device; }
@@ -226,6 +250,8 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
     if (d->gate_pending) fdev_gate_open(d, 1);
     for (int k = 0; k < nseg; k++) {
         const fdev_seg *s = &segs[k];
+        int pre = s->out2 && s->out2_pre && s->kind != FDEV_COPY;
+        if (pre) memmove(s->out2, s->x, s->n * esz(dtype)); /* the pre-image, before an in-place reduce */
         if (s->kind == FDEV_COPY) {
             memmove(s->out, s->x, s->n * esz(dtype));
         } else {
@@ -236,7 +262,7 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
             default: LOOP(double, op_f64); break;
             }
         }
-        if (s->out2) memmove(s->out2, s->out, s->n * esz(dtype));
+        if (s->out2 && !pre) memmove(s->out2, s->out, s->n * esz(dtype));
         if (s->remote & FDEV_REMOTE_OUT) d->ctr.link_bytes += (double)s->n * (double)esz(dtype);
     }
     d->ctr.launches[tag]++;
@@ -304,7 +330,26 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
 static int can_gate(const ftar_dev *d)
 {
     const char *e = getenv("FTAR_HOSTSIM_GATE");
-    return !(e && !atoi(e)) && !d->profiling && !d->gate_pending;
+    return !(e && !atoi(e)) && !d->profiling && !d->gate_pending && d->flag_sync;
+}
+
+/* TEST-ONLY (FTAR_HOSTSIM_GATE_CORRUPT=1): a gated launch that runs gets its first output
+ * element wrong -- the stand-in for a gated path that is not exact on some hardware, which
+ * bench.py's exactness leg must catch and route around (tests/test_bench_logic.py) */
+static void corrupt_gated(ftar_dev *d)
+{
+    const char *e = getenv("FTAR_HOSTSIM_GATE_CORRUPT");
+    if (!e || !atoi(e)) return;
+    size_t n = d->gated.batch ? d->gated.n[0] : d->gated.segs[0].n;
+    void *outs[2] = {d->gated.batch ? d->gated.out[0] : d->gated.segs[0].out, d->gated.batch ? NULL : d->gated.segs[0].out2};
+    for (int k = 0; k < 2; k++) {
+        void *o = outs[k];
+        if (!o || !n) continue;
+        if (d->gated.dtype == 0) ((int32_t *)o)[0] += 1;
+        else if (d->gated.dtype == 1) ((float *)o)[0] += 1.0f;
+        else if (d->gated.dtype == 2) ((int64_t *)o)[0] += 1;
+        else ((double *)o)[0] += 1.0;
+    }
 }
 
 int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc,
@@ -366,9 +411,11 @@ int fdev_gate_open(ftar_dev *d, int skip)
         return 0;
     }
     d->gates_run++;
-    if (!d->gated.batch) return fdev_run(d, d->gated.dtype, d->gated.op, d->gated.segs, d->gated.nseg, d->gated.tag);
-    return fdev_tree_batch(d, d->gated.dtype, d->gated.op, d->gated.src, d->gated.nsrc, d->gated.remote, d->gated.out,
-                           d->gated.n, d->gated.ntree, d->gated.tag);
+    int rc = d->gated.batch ? fdev_tree_batch(d, d->gated.dtype, d->gated.op, d->gated.src, d->gated.nsrc, d->gated.remote,
+                                              d->gated.out, d->gated.n, d->gated.ntree, d->gated.tag)
+                            : fdev_run(d, d->gated.dtype, d->gated.op, d->gated.segs, d->gated.nseg, d->gated.tag);
+    corrupt_gated(d);
+    return rc;
 }
 
 int fdev_gate_pending(const ftar_dev *d) { return d->gate_pending; }

@@ -14,12 +14,14 @@
  *      FTAR_PROBE_INPLACE=1 (send buffer = receive buffer),
  *      FTAR_PROBE_OFFSET=k (buffers start k elements past a 16-byte boundary),
  *      FTAR_PROBE_PINNED=1 (buffers from hipHostMalloc, looked up in the loaded HIP runtime:
- *      the _host entry points then run zero copy; host-sim build: no runtime, plain memory)
+ *      the _host entry points then run zero copy; host-sim build: no runtime, plain memory),
+ *      FTAR_PROBE_SLEEP_US=t (sleep before every call: a late rank, with FTAR_PROBE_RANK_ENV)
  */
 #include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "ftar.h"
 
@@ -96,6 +98,8 @@ int main(void)
             src = out;
         }
         int rd = !strcmp(algo, "rd"), rc;
+        /* FTAR_PROBE_SLEEP_US (with FTAR_PROBE_RANK_ENV: one rank): arrive late at every call */
+        if (getenv("FTAR_PROBE_SLEEP_US")) usleep((useconds_t)atoll(getenv("FTAR_PROBE_SLEEP_US")));
         if (dev)
             rc = rd ? ftar_recursive_doubling(src, out, count, (ftar_dtype)dt, (ftar_op)op, comm)
                     : ftar_allreduce_rabenseifner(src, out, count, (ftar_dtype)dt, (ftar_op)op, comm);
@@ -114,9 +118,10 @@ int main(void)
         fclose(f);
         snprintf(path, sizeof(path), "%s/status_%d_%d.txt", dir, rank, it);
         f = fopen(path, "w");
-        fprintf(f, "%d %d %d %d %lld %lld %lld %d %d %d %d %d\n", rc, crank, csize, st.recoveries,
+        fprintf(f, "%d %d %d %d %lld %lld %lld %d %d %d %d %d %d %d %d\n", rc, crank, csize, st.recoveries,
                 (long long)(st.wall_s * 1e6), (long long)(st.sync_wait_s * 1e6), (long long)(st.drain_s * 1e6), st.syncs,
-                st.relayed_steps, st.mesh_steps, st.gated_launches, st.gated_skips);
+                st.relayed_steps, st.mesh_steps, st.gated_launches, st.gated_skips, st.step0_copy, st.gate_holds,
+                st.gate_relaunches);
         fclose(f);
     }
     ftar_finalize(comm);

@@ -79,22 +79,48 @@ def test_c5_leg_summary(bench):
     assert res["recovered_rs"] and res["recovered_ag"] and res["recovered_ag_call_ms"] == 3.5
     assert res["kill_ag"].startswith("6:2:1:3 in call 2")
     runs = [json.loads(l) for l in open(tmp / "log.jsonl")]
-    # both recovery shapes: the default, then the reference's (FTAR_REDUNDANCY=1)
+    # both recovery shapes: the library's default (auto: the ranks span GPUs, so the
+    # reference's step-0 copy moves), then the opt-in elided shape (FTAR_REDUNDANCY=0)
     assert [r["kill"] for r in runs] == [None, "6:1:1:3:2", "6:2:1:3:2"] * 2
-    assert [r["redundancy"] for r in runs] == [None] * 3 + ["1"] * 3
+    assert [r["redundancy"] for r in runs] == [None] * 3 + ["0"] * 3
     assert runs[0]["argv"][-3:] == ["raben", "1024", "6"]
-    ref = res["reference_shape"]
-    assert ref["recovered"] and ref["recovered_rs"] and ref["recovered_ag"], ref
-    assert ref["no_fault"]["survivors"] == 9 and ref["fault"]["survivors"] == 8
+    assert "span GPUs" in res["recovery_shape"] and "reference_shape" not in res
+    el = res["elided_shape"]
+    assert el["recovered"] and el["recovered_rs"] and el["recovered_ag"], el
+    assert el["no_fault"]["survivors"] == 9 and el["fault"]["survivors"] == 8
+    assert res["dead_input_cross_device"] == el["dead_input_cross_device"] == "recovered"
+
+
+def test_c5_leg_elided_shape_abort_is_reported(bench):
+    """On the node the elided shape's RS-kill job decides whether a dead process's memory
+    stays readable across GPUs: an MPI_Abort there reads `dead_input_cross_device: abort`
+    (the default shape, with the copy, still recovers)."""
+    m, tmp = bench
+    f = tmp / "fault-tolerant_amd" / "bin" / "ftrun"
+    f.write_text(FAKE_FTRUN.replace("if kill:\n    sys.stderr.write(",
+                                    "if kill and os.environ.get('FTAR_REDUNDANCY') == '0' and kill.split(':')[1] == '1':\n"
+                                    "    sys.stderr.write('MPI_ABORT was invoked on rank 1\\n'); sys.exit(1)\n"
+                                    "if kill:\n    sys.stderr.write(")
+                 .replace("for r in range(n):\n    if r == victim:",
+                          "for r in range(n):\n    if kill and os.environ.get('FTAR_REDUNDANCY') == '0' and "
+                          "kill.split(':')[1] == '1':\n        break\n    if r == victim:"))
+    res = m.c5_leg(8, list(range(8)), 1024, 9, _deadline())
+    assert res["recovered"] is True, res
+    assert res["dead_input_cross_device"] == "abort", res["elided_shape"]["fault"]
 
 
 def test_c5_leg_rehearsal_layout(bench):
-    """One GPU, 5 ranks (FTAR_C5_RANKS): the victim is the last rank."""
-    m, _ = bench
+    """One GPU, 5 ranks (FTAR_C5_RANKS): the victim is the last rank; the default is the
+    elided shape there, the other shape the reference's copy."""
+    m, tmp = bench
     res = m.c5_leg(2, [0], 64, 5, _deadline())
     assert res["devmap"] == [0, 0, 0, 0, 0] and res["kill"].startswith("4:1:1:3 in call 2")
     assert res["kill_ag"].startswith("4:2:0:3 in call 2")  # two AG steps: the last one recovers
     assert res["recovered"] is True, res
+    assert "one GPU" in res["recovery_shape"] and res["reference_shape"]["recovered"]
+    assert "dead_input_cross_device" not in res
+    runs = [json.loads(l) for l in open(tmp / "log.jsonl")]
+    assert [r["redundancy"] for r in runs] == [None] * 3 + ["1"] * 3
 
 
 def test_c5_leg_wrong_sum_is_not_recovered(bench, monkeypatch):
@@ -190,25 +216,56 @@ def test_side_leg_past_its_deadline_is_recorded(bench, monkeypatch):
     assert seen and 0 < seen[0] <= 8.0 * 0.65 + 0.5  # the campaign runs on what is left
 
 
-def test_north_star_block_prices():
-    """SURVEY.md 8d: FT Raben moves 2.25 S per rank and direction at p = 8 over one link per
-    step; at B_link = 153.6 GB/s t_roof = 3.93 ms and the 70 % target is algbw >= 47.8 GB/s."""
+def _bench_module():
     spec = importlib.util.spec_from_file_location("bench_ns", os.path.join(ROOT, "bench.py"))
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
+    return m
+
+
+def _fracs(d):
+    """Every value under a key named `frac` or ending in `_frac`, recursively."""
+    out = []
+    for k, v in d.items():
+        if isinstance(v, dict):
+            out += _fracs(v)
+        elif k == "frac" or k.endswith("_frac"):
+            out.append(v)
+    return out
+
+
+def test_north_star_block_prices():
+    """SURVEY.md 8d: FT Raben moves 2.25 S per rank and direction at p = 8 over one link per
+    step; at B_link = 153.6 GB/s t_roof = 3.93 ms and the 70 % target is algbw >= 47.8 GB/s.
+    The top-level fraction is the timed schedule against its OWN bound: the
+    one-hop mesh moves 2 S / 8 over each link, 0.874 ms at 76.8 GB/s."""
+    m = _bench_module()
     S = 256 << 20
-    ns = m.north_star_block(8, S, 5.0e-3, "mesh", None, 7, 2.0 * S / 8)
+    # a synthetic node line: mesh 1.3 ms, the reference's shape 9 ms, calibrated link 76.8 GB/s
+    ns = m.north_star_block(8, S, 1.3e-3, "mesh", 76.8, 7, 2.0 * S / 8, t_ref=9e-3)
+    assert ns["basis"] == "calibrated" and ns["applies"]
+    t_sched = 2.0 * S / 8 / 76.8e9
+    assert ns["frac"] == round(t_sched / 1.3e-3, 4) and ns["met"] is False  # 0.672 < 0.70
+    t_roof = 2.25 * S / 76.8e9
+    assert ns["reference_schedule_frac"] == round(t_roof / 9e-3, 4) and ns["reference_schedule_met"] is True
+    assert ns["speedup_vs_survey_roofline"] == round(t_roof / 1.3e-3, 4) > 1  # a speed-up, not a fraction
+    assert all(f is None or f <= 1.0 for f in _fracs(ns)), _fracs(ns)
     row = ns["priced"]["survey_153.6_assumed"]
-    assert abs(row["t_roof_ms"] - 3.9322) < 1e-3 and abs(row["target_algbw_GBps"] - 47.78) < 0.05
-    assert ns["basis"] == "survey_153.6_assumed" and ns["frac"] == round(3.9322e-3 / 5.0e-3, 4)
-    assert ns["met"] is True and ns["applies"]
-    assert abs(ns["priced"]["nominal_76.8_assumed"]["t_roof_ms"] - 7.8643) < 1e-3
-    cal = m.north_star_block(8, S, 5.0e-3, "mesh", 60.0, 7, 2.0 * S / 8, t_ref=12e-3)
-    assert cal["basis"] == "calibrated"
-    t_roof = 2.25 * S / 60e9
-    assert cal["frac"] == round(t_roof / 5e-3, 4) and cal["met"] == (t_roof / 5e-3 >= 0.7)
-    assert cal["priced"]["calibrated"]["reference_shape"]["frac"] == round(t_roof / 12e-3, 4)
-    assert cal["priced"]["calibrated"]["schedule_t_roof_ms"] == round(2.0 * S / 8 / 60e9 * 1e3, 4)
+    assert abs(row["survey_t_roof_ms"] - 3.9322) < 1e-3 and abs(row["survey_target_algbw_GBps"] - 47.78) < 0.05
+    assert abs(ns["priced"]["nominal_76.8_assumed"]["survey_t_roof_ms"] - 7.8643) < 1e-3
+    # met follows the schedule's own fraction
+    fast = m.north_star_block(8, S, 1.2e-3, "mesh", 76.8, 7, 2.0 * S / 8)
+    assert fast["met"] is True and fast["frac"] == round(t_sched / 1.2e-3, 4)
+    # a time below its own bound (the reference's shape in 6 ms, faster than 2.25 S over one
+    # 76.8 GB/s link allows): no fraction above 1 is claimed, the price is flagged instead
+    bad = m.north_star_block(8, S, 1.3e-3, "mesh", 76.8, 7, 2.0 * S / 8, t_ref=6e-3)
+    assert bad["reference_schedule_frac"] is None and bad["reference_schedule_met"] is None
+    assert bad["priced"]["calibrated"]["reference_schedule"]["frac_raw"] > 1
+    assert all(f is None or f <= 1.0 for f in _fracs(bad)), _fracs(bad)
+    # no calibration: priced at SURVEY's 153.6 GB/s assumption (the strictest)
+    nocal = m.north_star_block(8, S, 5.0e-3, "mesh", None, 7, 2.0 * S / 8)
+    assert nocal["basis"] == "survey_153.6_assumed"
+    assert nocal["frac"] == round(2.0 * S / 8 / 153.6e9 / 5.0e-3, 4)
     reh = m.north_star_block(2, S, 1e-3, "mesh-oneshot", None, 1, S, rehearsal=True)
     assert reh["frac"] is None and reh["met"] is None and reh["rehearsal"]
 
@@ -252,7 +309,7 @@ def test_bench_multi_headline_survives_hung_and_failing_legs(hostsim, tmp_path):
             assert k in d, k
         assert d["value"] > 0 and d["n_gpus"] == 2 and "CPU TEST" in d["data"]
         ns = d["north_star"]
-        assert ns["target"] and ns["priced"]["survey_153.6_assumed"]["t_roof_ms"] > 0 and "met" in ns
+        assert ns["target"] and ns["priced"]["survey_153.6_assumed"]["survey_t_roof_ms"] > 0 and "met" in ns
     assert head["value"] == fin["value"]
     assert fin["side_legs"]["c5"]["status"] == "timeout" and "killed" in fin["c5_single_kill"]["error"]
     assert fin["side_legs"]["total_s"] <= 20 + 2
@@ -266,6 +323,36 @@ def test_bench_multi_headline_survives_hung_and_failing_legs(hostsim, tmp_path):
     sweep = fin["size_sweep_us"]
     assert sweep[str(8 * 65536)]["raben_us"] > 0 and sweep[str(8 * 65536)]["rd_us"] > 0, sweep
     assert took < 150, took
+
+
+@pytest.mark.timeout(240)
+def test_bench_multi_small_call_fallback(hostsim, tmp_path):
+    """exact_on_node covers every small-call mechanism on both sides of its ~1 MiB threshold,
+    gated and ungated.  With a gated path that is not exact
+    (FTAR_HOSTSIM_GATE_CORRUPT: a gated launch's first output element is off by one), the
+    gated checks fail, the leg reruns them with the gates off, finds them exact, keeps that
+    setting for the rest of the job and records it; the size sweep is timed with it."""
+    cp, lines, took = _torchrun_cpu(tmp_path, {"FTAR_HOSTSIM_GATE_CORRUPT": "1"},
+                                    ["--side-budget", "5", "--no-c5", "--no-xgmi", "--no-cpu-baseline"], 200)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    fin = lines[-1]
+    ex = fin["exact_on_node"]
+    assert not ex["all_exact"], ex
+    fb = ex["small_call_fallback"]
+    assert fb["setting"] == "gate=0" and fb["tried"][0] == {"setting": "gate=0", "exact": True,
+                                                             "still_inexact": []}, fb
+    # the gated small checks, and every check of the job's own 256 KiB vector that is gated
+    # too (RD at a power of two, the one-shot mesh forms) -- never an ungated one
+    assert "rd_4B_gated" in fb["failed"] and not any(n.endswith("_ungated") for n in fb["failed"]), fb
+    assert ex["all_exact_after_fallback"] is True, ex
+    for label in ("4B", "4KiB", "64KiB", "1MiB-16B", "1MiB", "1MiB+16B"):  # --count 65536 = 256 KiB: 4 MiB skipped
+        for algo in ("raben", "rd"):
+            assert f"{algo}_{label}_ungated" in ex or 4 * {"4B": 1, "4KiB": 1024, "64KiB": 16384}.get(label, 1 << 30) \
+                > 4 * 65536, (algo, label)
+    assert ex["rd_4B_ungated"] and not ex["rd_4B_gated"]
+    sweep = fin["size_sweep_us"]
+    assert sweep["small_call_setting"] == "gate=0" and sweep["gate"] == 0, sweep
+    assert fin["transport_selection"]["inexact"], fin["transport_selection"]  # the gated one-shot failed there too
 
 
 @pytest.mark.timeout(240)

@@ -37,10 +37,12 @@ def test_bench_single_gpu_line():
               "dtype", "config", "roofline"):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 10 and d["roofline"]["bound"] == "hbm"
-    # within 10 % of the committed profile's fraction (the kernel sits at ~0.82 of 8 TB/s)
-    with open(os.path.join(ROOT, "profiles", "r03", "bench_n1.json")) as f:
-        committed = json.loads([l for l in f.read().splitlines() if l.startswith("{")][-1])["roofline"]["frac"]
-    assert abs(d["roofline"]["frac"] - committed) <= 0.10 * committed, (d["roofline"], committed)
+    # a fixed floor: 0.9 x the driver-observed 0.80 of 8 TB/s (boxes differ by a few %; the
+    # kernel sits at the measured streaming ceiling)
+    assert d["roofline"]["frac"] >= 0.72, d["roofline"]
+    # the PMC traffic is labelled with where it was measured (not by this run)
+    src = d["roofline"]["traffic_source"]
+    assert src["measured_in_this_run"] is False and src["file"] == "profiles/pmc_summary.json", src
     assert "rotating" in d["config"]["buffers"]
 
 
@@ -63,7 +65,7 @@ def test_bench_two_rank_scale_path():
     d = lines[-1]
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     ns = d["north_star"]  # present in a rehearsal too, fractions withheld (no link in the path)
-    assert ns["rehearsal"] and ns["frac"] is None and ns["priced"]["survey_153.6_assumed"]["t_roof_ms"] > 0
+    assert ns["rehearsal"] and ns["frac"] is None and ns["priced"]["survey_153.6_assumed"]["survey_t_roof_ms"] > 0
     assert all(v["status"] == "ok" for k, v in d["side_legs"].items() if isinstance(v, dict)), d["side_legs"]
     assert all(v["status"] == "ok" for v in d["legs"].values() if v["status"] != "skipped"), d["legs"]
     assert d["int32_rank_checksum_ok"] == {"raben": True, "rd": True}

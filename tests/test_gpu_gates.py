@@ -1,0 +1,54 @@
+"""GPU: launches queued behind gates when a peer is late (ADVICE r03, high + medium + low).
+
+A gated launch (Raben's one-shot, every RD step at a power of two, <= 1 MiB) is queued
+before the barrier that readies its operands and spins at the head of the rank's stream
+until the host opens its gate.  A late peer must cost neither the job nor a bounded stall:
+  * the host gives the gated launch up once its barrier waited FTAR_GATE_HOLD_US (the step
+    then launches after the barrier) -- `gate_holds`;
+  * with the host hold off, the device gives the gate up after FTAR_GATE_TIMEOUT_MS (its
+    workgroups return without touching memory) and the next drain relaunches the plan
+    ungated -- `gate_relaunches` -- instead of failing the call; for RD that drain is the one
+    with step s + 1 already queued behind its own gate (the verify the gate-pending branch
+    used to skip).
+Every result bit-exact against the oracle.  All ranks on GPU 0 of the test box.
+"""
+import numpy as np
+import pytest
+
+import harness as H
+
+pytestmark = pytest.mark.gpu
+
+ALL_ON_GPU0 = ",".join(["0"] * 16)
+
+
+def _run(oracle, algo, p, env, iters=3, count=1031):
+    ins = oracle.random_inputs(p, count, seed=p + 17)
+    o = oracle.rabenseifner(ins) if algo == "raben" else oracle.recursive_doubling(ins)
+    late = {"FTAR_PROBE_RANK_ENV": f"{p - 1}:FTAR_PROBE_SLEEP_US=300000"}
+    r = H.run_probe(algo, ins, iters=iters, backend="gpu", devmap=ALL_ON_GPU0, timeout=120, env_extra=dict(late, **env))
+    assert r.returncode == 0 and not r.aborted, r.stderr[-2000:]
+    for w in range(p):
+        for it in range(iters):
+            assert r.status[w][it][0] == 0, r.status[w]
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+    return r
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("algo,p", [("raben", 4), ("rd", 4), ("rd", 2)])
+def test_late_peer_host_gives_gate_up(oracle, algo, p):
+    r = _run(oracle, algo, p, {"FTAR_GATE_HOLD_US": "2000"})
+    # call 0 allocates the workspace, whose collective absorbs the late arrival before any gate
+    assert all(r.status[w][it][13] >= 1 for w in range(p - 1) for it in (1, 2)), r.status
+    assert all(r.status[w][it][14] == 0 for w in range(p) for it in range(3)), r.status  # no device timeout
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("algo,p", [("raben", 4), ("rd", 4), ("rd", 2)])
+def test_late_peer_device_gate_timeout_relaunches(oracle, algo, p):
+    r = _run(oracle, algo, p, {"FTAR_GATE_HOLD_US": "0", "FTAR_GATE_TIMEOUT_MS": "30"})
+    assert all(r.status[w][it][13] == 0 for w in range(p) for it in range(3)), r.status  # the host never gave up
+    # the waiting ranks' gated launches timed out on the device and were relaunched
+    assert all(r.status[w][2][14] >= 1 for w in range(p - 1)), r.status
+    assert "relaunched" in r.stderr, r.stderr[-1500:]

@@ -276,22 +276,24 @@ def test_torch_device_buffers(oracle, algo, p, mode):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
-@pytest.mark.parametrize("push", ["0", "1", "2"])
+@pytest.mark.parametrize("push,unroll", [("0", "1"), ("1", "1"), ("2", "1"), ("0", "2"), ("0", "4"), ("1", "4")])
 @pytest.mark.parametrize("p,op,count", [(2, 0, 100003), (4, 0, 100003), (8, 0, 65536 + 5), (4, 2, 4099), (8, 3, 4099),
                                         (4, 0, (1 << 22) + 13), (8, 1, (1 << 20) + 3)])
-def test_mesh_schedule(oracle, p, op, count, push):
+def test_mesh_schedule(oracle, p, op, count, push, unroll):
     """Power of two without a spare: one-hop reduce-scatter -- a tree kernel over p - 1
     peer pulls, or (FTAR_PUSH=1) p - 1 remote-store copies into the owners followed by the
     owner's tree over local memory -- and allgather (FTAR_PUSH=2: the owner's tree also
     stores its block into every peer), bit-identical to the step-by-step schedule; MAX/MIN
-    with NaN and signed zeros pin the operand order of every combination."""
+    with NaN and signed zeros pin the operand order of every combination.  FTAR_TREE_UNROLL
+    = 2 / 4 (vectors per lane and source, p = 4, 8): the same tree per element, same bits --
+    ragged lengths exercise the partial last workgroup and the scalar tail."""
     dt = np.int32 if op == 1 else np.float32
     ins = oracle.random_inputs(p, count, seed=p * 7 + op, dtype=dt)
     if op >= 2:
         ins = H.with_specials(ins, p + op)
     # one device-resident call (the host pipeline would split >= 16 MiB into chunk calls)
     o, r = _check(oracle.rabenseifner, "raben", ins, op=op,
-                  env={"FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0", "FTAR_PUSH": push})
+                  env={"FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0", "FTAR_PUSH": push, "FTAR_TREE_UNROLL": unroll})
     assert all(st[0][9] == 2 for st in r.status.values()), r.status
 
 

@@ -162,6 +162,30 @@ def test_rd_repeated_calls_after_recovery(hostsim, oracle, p):
                 assert st[10:12] == (n.bit_length() - 1, 0), st
 
 
+@pytest.mark.parametrize("algo,p", [("rd", 4), ("raben", 4), ("rd", 8)])
+def test_late_peer_gives_the_gate_up(hostsim, oracle, algo, p):
+    """A peer that arrives late (here 300 ms) at a call whose small launches are queued
+    behind gates: the waiting ranks' barrier passes FTAR_GATE_HOLD_US, so they give their
+    gated launch up (the stream is not held by it any longer) and launch after
+    the barrier instead -- every result exact, and the give-up counted (gate_holds).  With
+    FTAR_GATE_HOLD_US=0 the gate is never given up by the host."""
+    ins = oracle.random_inputs(p, 1031, seed=p + 5)
+    o = _fn(oracle, algo)(ins)
+    late = {"FTAR_PROBE_RANK_ENV": f"{p - 1}:FTAR_PROBE_SLEEP_US=300000", "FTAR_GATE_HOLD_US": "2000"}
+    r = H.run_probe(algo, ins, backend="hostsim", iters=3, env_extra=late)
+    assert r.returncode == 0, r.stderr[-1000:]
+    for w in range(p):
+        for it in range(3):
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+    # (call 0 allocates the workspace: its collective absorbs the late arrival before any gate)
+    holds = [r.status[w][it][13] for w in range(p - 1) for it in (1, 2)]
+    assert all(h >= 1 for h in holds), r.status
+    r = H.run_probe(algo, ins, backend="hostsim", iters=2, env_extra=dict(late, FTAR_GATE_HOLD_US="0"))
+    assert r.returncode == 0 and all(r.status[w][it][13] == 0 for w in range(p) for it in range(2)), r.status
+    for w in range(p):
+        assert np.array_equal(r.outputs[w][1].view(np.uint32), o.outputs[w].view(np.uint32)), w
+
+
 def test_rd_after_raben_recovery(hostsim, oracle):
     """RD after a Raben recovery runs on the re-targeted comm order."""
     inputs = oracle.random_inputs(9, 777, seed=5)
@@ -796,16 +820,17 @@ def test_kill_logical_bitwise(hostsim, oracle, algo, p, kill, op):
 
 @pytest.mark.parametrize("p", [5, 9])
 def test_withdrawn_dead_input_aborts(hostsim, oracle, p):
-    """Without the step-0 redundancy copy (the default with a spare), the RS replay reads the
-    dead rank's step-0 input where it lies (deviation 6): a process death leaves
-    it mapped, a lost device does not.  FTAR_KILL_WITHDRAW makes the victim withdraw its input
-    as it dies (its workspace generation moves on, its published sbuf is retracted): the
-    replay must then refuse to read it and the job abort -- never a result from a stale or
-    unmapped buffer.  With the reference's copy (FTAR_REDUNDANCY=1) the same kills recover
-    bit-exact like the oracle, and reduce-scatter kills of the idle spare, which need no
-    replay, recover either way."""
+    """Without the step-0 redundancy copy (FTAR_REDUNDANCY=0, or the auto default on one GPU),
+    the RS replay reads the dead rank's step-0 input where it lies (deviation 6):
+    a process death leaves it mapped, a lost device does not.  FTAR_KILL_WITHDRAW makes the
+    victim withdraw its input as it dies (its workspace generation moves on, its published
+    sbuf is retracted): the replay must then refuse to read it and the job abort -- never a
+    result from a stale or unmapped buffer.  With the reference's copy (FTAR_REDUNDANCY=1)
+    the same kills recover bit-exact like the oracle, and reduce-scatter kills of the idle
+    spare, which need no replay, recover either way."""
     ins = oracle.random_inputs(p, 257, seed=p + 7)
     n_abort = n_rec = 0
+    elided = {"FTAR_KILL_WITHDRAW": "1", "FTAR_REDUNDANCY": "0"}
     for v in range(p):
         for st in (1, 2):
             for pt in range(4):
@@ -814,13 +839,50 @@ def test_withdrawn_dead_input_aborts(hostsim, oracle, p):
                 if o.aborted or o.status[v] != oracle.DEAD:
                     continue
                 replay = v != 1  # rank 1 is the idle odd rank of the pre-step pair (rem = 1)
-                r = H.run_probe("raben", ins, ks, backend="hostsim", env_extra={"FTAR_KILL_WITHDRAW": "1"})
+                r = H.run_probe("raben", ins, ks, backend="hostsim", env_extra=elided)
                 if replay:
                     assert r.aborted and not r.outputs, (ks, r.stderr[-800:])
                     assert "not readable" in r.stderr, r.stderr[-800:]
                     n_abort += 1
                 else:
-                    _cmp(oracle.rabenseifner, "raben", ins, ks, env={"FTAR_KILL_WITHDRAW": "1"})
+                    _cmp(oracle.rabenseifner, "raben", ins, ks, env=elided)
                     n_rec += 1
                 _cmp(oracle.rabenseifner, "raben", ins, ks, env={"FTAR_KILL_WITHDRAW": "1", "FTAR_REDUNDANCY": "1"})
     assert n_abort > 0 and n_rec > 0, (n_abort, n_rec)
+
+
+@pytest.mark.parametrize("p", [5, 9])
+def test_redundancy_auto_follows_the_devmap(hostsim, oracle, p):
+    """FTAR_REDUNDANCY unset (auto): with a spare, the step-0 copy moves when the comm spans
+    more than one GPU -- so a replay never depends on a dead process's memory staying
+    readable across devices (the reference copies at step 0 because that memory is gone,
+    raben/rabenseifner.c:206-211) -- and is elided when every rank shares one GPU (where a
+    peer's mapping provably keeps it).  Two-device devmap: every replaying kill recovers
+    bit-exact against the oracle even when the victim withdraws its input as it dies; one
+    device: the copy is elided (step0_copy 0) and the same withdrawn input aborts."""
+    ins = oracle.random_inputs(p, 257, seed=p + 9)
+    two = ",".join(str(r % 2) for r in range(p))
+    one = ",".join("0" for _ in range(p))
+    n = 0
+    for v in range(2, p):  # ranks whose death needs the impersonation replay
+        ks = [(v, 1, 1, 3)]  # reduce-scatter step 1, mid-exchange
+        o = oracle.rabenseifner(ins, ks)
+        if o.aborted or o.status[v] != oracle.DEAD:
+            continue
+        r = H.run_probe("raben", ins, ks, backend="hostsim", devmap=two, env_extra={"FTAR_KILL_WITHDRAW": "1"})
+        assert not r.aborted, (ks, r.stderr[-800:])
+        for w, s in enumerate(o.status):
+            if s == 0:
+                assert np.array_equal(r.outputs[w][0].view(np.uint32), o.outputs[w].view(np.uint32)), (ks, w)
+                assert r.status[w][0][12] == 1, r.status[w][0]  # the copy moved
+        r1 = H.run_probe("raben", ins, ks, backend="hostsim", devmap=one, env_extra={"FTAR_KILL_WITHDRAW": "1"})
+        assert r1.aborted and "not readable" in r1.stderr, (ks, r1.stderr[-800:])
+        n += 1
+    assert n > 0
+    r = H.run_probe("raben", ins, backend="hostsim", devmap=one)
+    assert all(r.status[w][0][12] == 0 for w in range(p)), r.status
+    r = H.run_probe("raben", ins, backend="hostsim", devmap=two)
+    assert all(r.status[w][0][12] == 1 for w in range(p)), r.status
+    # power of two (no spare): no handler can use the copy, whatever the layout
+    r = H.run_probe("raben", ins[:4], backend="hostsim", devmap="0,1,2,3")
+    assert all(r.status[w][0][12] == 0 for w in range(4)), r.status

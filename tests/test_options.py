@@ -32,9 +32,12 @@ def _get(L, h, opt):
 def test_option_defaults_and_roundtrip(solo):
     L, h = solo
     # defaults: overlap on, relay on (4 MiB threshold), loop stretch off, copy engine off,
-    # redundancy only where a spare can use it
-    assert [_get(L, h, o) for o in range(6)] == [1.0, 1.0, float(4 << 20), 0.0, 0.0, 0.0]
-    for opt, val in ((0, 0), (1, 0), (2, 1 << 20), (3, 0.5), (4, 1), (5, 1)):
+    # redundancy auto (2: the step-0 copy moves where a spare exists and the comm spans GPUs)
+    assert [_get(L, h, o) for o in range(6)] == [1.0, 1.0, float(4 << 20), 0.0, 0.0, 2.0]
+    # flag-signalled drains on, tree kernel one vector per lane and source
+    assert _get(L, h, 10) == 1.0 and _get(L, h, 11) == 1.0
+    for opt, val in ((0, 0), (1, 0), (2, 1 << 20), (3, 0.5), (4, 1), (5, 1), (5, 0), (5, 2), (10, 0), (10, 1),
+                     (11, 2), (11, 4), (11, 1)):
         assert L.ftar_comm_set_option(h, opt, val) == 0
         assert _get(L, h, opt) == val
 
@@ -44,5 +47,8 @@ def test_option_errors(solo):
     assert L.ftar_comm_set_option(h, 99, 1) == 13       # FTAR_ERR_ARG
     assert L.ftar_comm_set_option(h, 2, -1) == 13
     assert L.ftar_comm_set_option(None, 0, 1) == 13
+    assert L.ftar_comm_set_option(h, 5, 3) == 13        # redundancy: 0 never, 1 always, 2 auto
+    assert L.ftar_comm_set_option(h, 11, 3) == 13       # tree unroll: 1, 2 or 4
+    assert L.ftar_comm_set_option(h, 11, 2.5) == 13
     v = ctypes.c_double()
     assert L.ftar_comm_get_option(h, 99, ctypes.byref(v)) == 13
