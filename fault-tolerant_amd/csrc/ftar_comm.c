@@ -161,6 +161,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->push = getenv("FTAR_PUSH") ? atoi(getenv("FTAR_PUSH")) : 0;
     c->gate = getenv("FTAR_GATE") ? atoi(getenv("FTAR_GATE")) != 0 : 1;
     c->gate_hold_s = (getenv("FTAR_GATE_HOLD_US") ? atof(getenv("FTAR_GATE_HOLD_US")) : 2000.0) * 1e-6;
+    c->gate_max = getenv("FTAR_GATE_MAX") ? (size_t)atoll(getenv("FTAR_GATE_MAX")) : ((size_t)16 << 20);
     c->oneshot_max = getenv("FTAR_ONESHOT_MAX") ? (size_t)atoll(getenv("FTAR_ONESHOT_MAX")) : ((size_t)1 << 20);
     c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
     c->stage_max = getenv("FTAR_STAGE_MAX") ? (size_t)atoll(getenv("FTAR_STAGE_MAX")) : ((size_t)1 << 20);

@@ -153,6 +153,14 @@ struct ftar_dev {
     } gp[2];
     int gate_relaunches;
     unsigned tree_unroll;          // FDEV_KNOB_TREE_UNROLL
+    // Mid-size gated launches (more workgroups than signal cheaply): queued behind a fenced
+    // marker (fence_pre) the drain before the barrier waits on, grid capped at big_blocks so a
+    // waiting launch holds a part of the device only, the gate relayed through device words
+    // (gate_dw: election words [0..7], verdict words [32..39], one per gate slot).
+    hipEvent_t fence_pre;
+    unsigned *gate_dw;
+    unsigned big_blocks;
+    int big_pending;               // the pending gated launch is a relayed (mid-size) one
 };
 
 extern "C" {
@@ -241,6 +249,20 @@ int fdev_open(int device, ftar_dev **out)
             }
             HIPCHK(hipDeviceSynchronize());
         }
+        d->fence_pre = nullptr;
+        d->gate_dw = nullptr;
+        d->big_pending = 0;
+        {
+            const char *bb = getenv("FTAR_GATE_BIG_BLOCKS");
+            long v = bb ? atol(bb) : (long)prop.multiProcessorCount / 2;
+            d->big_blocks = (unsigned)(v < 1 ? 1 : v);
+        }
+        if (d->flag_sync) {
+            HIPCHK(hipEventCreateWithFlags(&d->fence_pre, hipEventDisableTiming)); // fenced, see sync_stream
+            HIPCHK(hipMalloc((void **)&d->gate_dw, 256));
+            HIPCHK(hipMemset(d->gate_dw, 0, 256));
+            HIPCHK(hipDeviceSynchronize());
+        }
     }
     d->h2d = d->d2h = nullptr;
     d->fence_d2h = nullptr;
@@ -281,6 +303,8 @@ void fdev_close(ftar_dev *d)
     if (d->h2d) (void)hipStreamDestroy(d->h2d);
     if (d->sig_cnt) (void)hipFree(d->sig_cnt);
     if (d->sig_flag) (void)hipHostFree(d->sig_flag);
+    if (d->gate_dw) (void)hipFree(d->gate_dw);
+    if (d->fence_pre) (void)hipEventDestroy(d->fence_pre);
     delete d;
 }
 
@@ -739,6 +763,7 @@ int fdev_gate_open(ftar_dev *d, int skip)
         d->ctr.hbm_bytes += d->gate_hbm;
     }
     d->gate_pending = 0;
+    d->big_pending = 0;
     d->gate_verify = 1;
     d->verify_seq = d->gate_seq;
     return 0;
@@ -811,6 +836,38 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
     return run_on(d, d->stream, dtype, op, segs, nseg, tag);
 }
 
+// A mid-size launch (more workgroups than signal their completion cheaply) queued behind a
+// gate: a fenced marker is recorded first -- the drain before the barrier waits for it, i.e.
+// for everything queued before the gated launch, and its system-scope release makes that
+// work visible to the peers as the usual drain does -- then the launch, its grid capped at
+// big_blocks workgroups (each loops over its share of tiles: a waiting launch occupies a
+// part of the device, so ranks sharing a GPU still run), its gate relayed through device
+// words.  It does not signal: after the gate opens it is drained by a fenced marker.
+static int run_gated_relayed(ftar_dev *d, int dtype, int op, const ftar::SegIn *in, int nseg, size_t es, double link,
+                             double hbm, int *gated)
+{
+    if (!d->flag_sync || !d->gate_dw || d->profiling || d->gate_pending) return 0;
+    ftar::KSegList L;
+    unsigned grid = ftar::plan_segments(in, nseg, es, d->big_blocks, &L);
+    if (grid == 0) return 0;
+    L.nt_store = nt_store();
+    HIPCHK(hipEventRecord(d->fence_pre, d->stream)); // the work before the gate, released and drainable
+    d->need_acquire = 0;
+    L.sig = arm_gate(d, link, hbm);
+    d->signalled--; // arm_gate counted a signalled launch: this one drains through a marker
+    L.sig.cnt = nullptr;
+    L.sig.flag = nullptr;
+    L.sig.gate_poll = d->gate_dw + d->gate_seq % ftar::kGateSlots;
+    L.sig.gate_dev = d->gate_dw + 32 + d->gate_seq % ftar::kGateSlots;
+    keep_plan(d, 0, dtype, op, 0, grid, &L, nullptr);
+    hipError_t e = ftar::launch_segments(dtype, op, L, grid, d->stream);
+    if (e != hipSuccess) return set_err(e, "segment_kernel launch (gated, relayed)");
+    d->gate_pending = 1;
+    d->big_pending = 1;
+    *gated = 1;
+    return 0;
+}
+
 int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag, void *stage_dst,
                    const void *stage_src, size_t stage_n, int *gated)
 {
@@ -833,6 +890,8 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
         }
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
+    if (grid > d->flag_max && !stage_dst)
+        return run_gated_relayed(d, dtype, op, in, nseg, es, link, hbm, gated);
     if (!can_gate(d, grid)) return 0;
     L.nt_store = nt_store();
     unsigned stage_tag = 0;
@@ -1012,9 +1071,24 @@ static int verify_gate(ftar_dev *d, int (*poll)(void *), void *arg)
     return rc;
 }
 
+static int spin(hipEvent_t e, int (*poll)(void *), void *arg);
+
 int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 {
     int rc;
+    if (d->gate_pending && d->big_pending) {
+        // a mid-size launch waits on its closed gate: the fenced marker recorded just before
+        // it covers (and released) everything queued earlier
+        rc = spin(d->fence_pre, poll, arg);
+        d->need_acquire = 0;
+        d->pre_gate_any = 0;
+        d->signalled = d->force_fence = 0;
+        d->unsignalled = 1; // the gated launch, drained through a marker after its gate opens
+        if (rc) return rc;
+        rc = verify_gate(d, poll, arg);
+        if (rc) return rc;
+        return harvest(d);
+    }
     if (d->gate_pending) {
         // a launch waits on its closed gate: drain what was queued before it (all of it
         // signalled, the gated launch checked; nothing is queued behind it, see note_launch),

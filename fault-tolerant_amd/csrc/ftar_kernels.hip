@@ -136,7 +136,7 @@ __device__ __forceinline__ void st16(uint4 *p, uint4 v, unsigned nts)
 // flag after the last store.  The branch is uniform over the launch.
 __device__ __forceinline__ void signal_acquire(const KSignal &G)
 {
-    if (G.cnt && G.acquire) {
+    if ((G.cnt || G.gate) && G.acquire) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // system scope: drop cached remote lines
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -179,26 +179,49 @@ __device__ __forceinline__ void signal_stage(const KSignal &G)
 // between polls; the workgroup learns the verdict through LDS.  Uniform over the launch.
 // Gates take turns over kGateSlots words (ftar_kernels.h): a workgroup that starts late
 // still finds its own verdict after the host has opened the next gate.
+// Thread 0: wait until `word` (scope S) reaches the gate's value; skip (and report) past
+// `ticks` of the wall clock, or when the word already holds a later gate.
+template <int S>
+__device__ __forceinline__ unsigned gate_wait(const KSignal &G, const unsigned *word, unsigned long long ticks)
+{
+    const unsigned long long t0 = wall_clock64();
+    unsigned v;
+    for (;;) {
+        v = __hip_atomic_load(word, __ATOMIC_RELAXED, S);
+        if ((int)((v & ~1u) - (G.gate_val & ~1u)) >= 0) break;
+        if (wall_clock64() - t0 > ticks) { // the host never opened it: skip, report
+            __hip_atomic_store(G.err, G.gate_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            v = G.gate_val | 1u;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if ((v & ~1u) != G.gate_val) { // the slot already holds a later gate: never run blind
+        __hip_atomic_store(G.err, G.gate_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        v |= 1u;
+    }
+    return v;
+}
+
 __device__ __forceinline__ bool signal_gate(const KSignal &G)
 {
     if (!G.gate) return true;
     __shared__ unsigned go;
     if (threadIdx.x == 0) {
-        const unsigned long long t0 = wall_clock64();
         unsigned v;
-        for (;;) {
-            v = __hip_atomic_load(G.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if ((int)((v & ~1u) - (G.gate_val & ~1u)) >= 0) break;
-            if (wall_clock64() - t0 > G.gate_ticks) { // the host never opened it: skip, report
-                __hip_atomic_store(G.err, G.gate_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                v = G.gate_val | 1u;
-                break;
+        if (!G.gate_dev) {
+            v = gate_wait<__HIP_MEMORY_SCOPE_SYSTEM>(G, G.gate, G.gate_ticks);
+        } else {
+            // relayed: the first workgroup of this gate polls the host word (over PCIe) and
+            // relays the verdict through device memory; the others poll that (agent scope)
+            const unsigned old = __hip_atomic_fetch_max(G.gate_poll, G.gate_val, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if ((int)(old - G.gate_val) < 0) {
+                v = gate_wait<__HIP_MEMORY_SCOPE_SYSTEM>(G, G.gate, G.gate_ticks);
+                __hip_atomic_store(G.gate_dev, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                v = gate_wait<__HIP_MEMORY_SCOPE_AGENT>(G, G.gate_dev, 2 * G.gate_ticks);
             }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if ((v & ~1u) != G.gate_val) { // the slot already holds a later gate: never run blind
-            __hip_atomic_store(G.err, G.gate_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            v |= 1u;
         }
         go = (v & 1u) ? 0u : 1u;
     }

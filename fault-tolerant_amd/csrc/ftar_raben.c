@@ -436,12 +436,35 @@ static int rb_mesh_push_finish(rb_ctx *x, void *rbuf)
  * anywhere in a phase ends the job exactly as it would at that step's agree.  Every
  * step's kill points are still passed (the injected death lands in the same phase), and
  * each phase ends in the reference's agree + barrier. */
+/* The mesh allgather's one launch: this rank's final block W -> rbuf and every peer's final
+ * block, pulled out of its W, into rbuf (the operands are known before the reduce-scatter's
+ * barrier: the launch can be queued ahead of it, behind a gate). */
+static int rb_mesh_ag_segs(rb_ctx *x, void *rbuf, fdev_seg *segs)
+{
+    ftar_comm *c = x->c;
+    const int L = x->steps, p = x->adjsize, v = x->vrank;
+    int ns = 0;
+    segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, x->rindex[L - 1]), at(x, c->ws[WS_W], x->rindex[L - 1]), NULL,
+                            (size_t)x->rcount[L - 1], NULL};
+    for (int j = 1; j < p; j++) {
+        int u = v ^ j;
+        int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
+        rb_windows(u, x->count, L, ri, si, rc, sc);
+        void *PW = ftar_buf(c, c->order[rb_real(x, u)], WS_W);
+        segs[ns++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, rbuf, ri[L - 1]), at(x, PW, ri[L - 1]), NULL,
+                                (size_t)rc[L - 1], NULL};
+    }
+    return ns;
+}
+
 static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
 {
     ftar_comm *c = x->c;
     const int L = x->steps, p = x->adjsize, v = x->vrank;
     void *W = c->ws[WS_W];
     int64_t own0 = x->rindex[L - 1], own_n = x->rcount[L - 1];
+    fdev_seg segs[FDEV_MAX_SEGS];
+    int ns = 0;
 
     uint64_t newf;
     if (x->push) {
@@ -466,6 +489,10 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
+    /* up to FTAR_GATE_MAX: the allgather's launch queued right behind the tree, its gate
+     * opened where it would otherwise be launched (after the reduce-scatter's agree) */
+    ns = rb_mesh_ag_segs(x, rbuf, segs);
+    if (c->gate && x->count * x->es <= c->gate_max) ftar_prelaunch(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP, NULL, NULL, 0);
     ftar_launched(c, FTAR_PH_LOOP, 0); /* every step's DURING point: the one launch is in flight */
     for (int s = 1; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_DURING);
     ftar_drain(c);
@@ -482,18 +509,9 @@ allgather:
     /* allgather: every peer's final block into rbuf, this rank's own out of W */
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
     ftar_enter(c);
-    fdev_seg segs[FDEV_MAX_SEGS];
-    int ns = 0;
-    segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, own0), at(x, W, own0), NULL, (size_t)own_n, NULL};
-    for (int j = 1; j < p; j++) {
-        int u = v ^ j;
-        int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
-        rb_windows(u, x->count, L, ri, si, rc, sc);
-        void *PW = ftar_buf(c, c->order[rb_real(x, u)], WS_W);
-        segs[ns++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, rbuf, ri[L - 1]), at(x, PW, ri[L - 1]), NULL,
-                                (size_t)rc[L - 1], NULL};
-    }
-    ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
+    ns = rb_mesh_ag_segs(x, rbuf, segs);
+    if (c->gplan.valid || fdev_gate_pending(c->dev)) ftar_run_gated_or(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
+    else ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
     ftar_launched(c, FTAR_PH_AG, L - 1);
     for (int s = L - 2; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_DURING);
     ftar_drain(c);

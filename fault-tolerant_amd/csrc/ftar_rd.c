@@ -248,15 +248,19 @@ int ftar_recursive_doubling(const void *src, void *dst, size_t count, ftar_dtype
     for (int i = 0; i < pp; i++) x->active[i] = c->order[i];
     x->ninactive = size - pp;
     for (int i = pp; i < size; i++) x->inactive[i - pp] = c->order[i];
-    /* Small calls at a power of two (no pre-step): each step's launch is queued ahead of the
-     * barrier that readies its operands, behind a gate (ftar_prelaunch) -- step 0's right
-     * behind the staging copy (every rank stages a small input, so the partners' inputs
-     * will be in their IN), step s + 1's behind step s's (the accumulators alternate W, T,
-     * W, ... on every rank).  The step then runs it only if its own plan, made after the
-     * barrier, is the same (ftar_xfer_step); a recovery in between makes it a plain launch. */
-    int ahead = c->gate && staged && x->ninactive == 0 && pp >= 2 && bytes <= c->stage_max && !c->copy_engine;
+    /* Small and mid-size calls at a power of two (no pre-step): each step's launch is queued
+     * ahead of the barrier that readies its operands, behind a gate (ftar_prelaunch) -- step
+     * 0's right behind the staging copy (every rank stages a small input, so the partners'
+     * inputs will be in their IN), step s + 1's behind step s's (the accumulators alternate
+     * W, T, W, ... on every rank).  The step then runs it only if its own plan, made after
+     * the barrier, is the same (ftar_xfer_step); a recovery in between makes it a plain launch. */
+    /* Mid-size vectors (up to FTAR_GATE_MAX) queue steps 1.. ahead too -- their operands are
+     * the peers' accumulators, predictable -- while step 0 reads the peers' inputs, which
+     * only small staged calls can predict (a larger input is read in place, where the
+     * peer's mapping is known after the barrier only). */
+    int ahead = c->gate && x->ninactive == 0 && pp >= 2 && bytes <= c->gate_max && !c->copy_engine;
     int folded = 0; /* the staging copy rides in step 0's gated launch, ahead of its gate */
-    if (ahead && rd_plan_ahead(x, 1, WS_IN, WS_IN, FDEV_TAG_STEP0, &c->gnext)) {
+    if (ahead && staged && bytes <= c->stage_max && rd_plan_ahead(x, 1, WS_IN, WS_IN, FDEV_TAG_STEP0, &c->gnext)) {
         c->gnext.valid = 0;
         folded = ftar_prelaunch(c, c->gnext.dtype, c->gnext.op, c->gnext.segs, c->gnext.nseg, c->gnext.tag,
                                 c->ws[WS_IN], src, count);

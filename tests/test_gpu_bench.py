@@ -72,6 +72,17 @@ def test_bench_two_rank_scale_path():
     assert d["max_abs_err_vs_rccl"] < 1e-5
     ex = d["exact_on_node"]  # integer-valued float inputs, new per trial: bitwise exact
     assert ex["all_exact"] and ex["chosen"] and ex["reference_shape"] and ex["rd"] and ex["chosen_64KiB"], ex
+    # every small-call mechanism on both sides of its threshold, gated and ungated
+    for label in ("4B", "4KiB", "64KiB", "1MiB-16B", "1MiB", "1MiB+16B", "4MiB"):
+        for algo in ("raben", "rd"):
+            for g in ("gated", "ungated"):
+                assert ex[f"{algo}_{label}_{g}"] is True, (algo, label, g, ex)
+    assert "small_call_fallback" not in ex, ex
+    assert d["size_sweep_us"] == {} or d["size_sweep_us"].get("small_call_setting", "").startswith("default")
+    # the renamed north-star fields: the schedule's own bound, the reference's schedule, a speed-up
+    for k in ("frac", "met", "reference_schedule_frac", "reference_schedule_met", "speedup_vs_survey_roofline",
+              "frac_definition"):
+        assert k in ns, (k, ns)
     assert d["config"]["schedule"] and d["config"]["transport"] == d["transport"]
     assert d["reference_shape"]["ms_per_step"] > 0
     cpu = d["cpu_baseline"]
@@ -84,6 +95,8 @@ def test_bench_two_rank_scale_path():
     assert "mid-exchange" in c5["fault"].get("victim", ""), c5
     ref = c5["reference_shape"]  # the reference's recovery shape (FTAR_REDUNDANCY=1) recovers too
     assert ref["recovered"], ref
+    # one GPU: the auto default elides the step-0 copy, the reference's shape moves it
+    assert c5["no_fault"]["step0_copy"] == 0 and ref["no_fault"]["step0_copy"] == 1, (c5["no_fault"], ref["no_fault"])
     camp = c5["random_kill_campaign"]  # kill_procs.sh's random SIGKILL, seeded draws
     assert camp["draws_run"] == 3 and camp["wrong"] == 0 and camp["lost"] == 0, camp
     for rk in camp["runs"]:

@@ -25,7 +25,12 @@ ALL_ON_GPU0 = ",".join(["0"] * 16)
 def _run(oracle, algo, p, env, iters=3, count=1031):
     ins = oracle.random_inputs(p, count, seed=p + 17)
     o = oracle.rabenseifner(ins) if algo == "raben" else oracle.recursive_doubling(ins)
-    late = {"FTAR_PROBE_RANK_ENV": f"{p - 1}:FTAR_PROBE_SLEEP_US=300000"}
+    # the last rank is late: small calls -- it arrives 300 ms late (its calls' first barrier
+    # has the gated launch pending); mid-size calls -- it stretches its steps to 300 ms
+    # (FTAR_LOOP_SECONDS: the barriers of steps 1.. / the reduce-scatter's agree, behind which
+    # the next launch is gated)
+    late = {"FTAR_PROBE_RANK_ENV": f"{p - 1}:FTAR_PROBE_SLEEP_US=300000" if count <= 4096 else
+            f"{p - 1}:FTAR_LOOP_SECONDS=0.3", "FTAR_RELAY": "0", "FTAR_HOST_PIPE": "0"}
     r = H.run_probe(algo, ins, iters=iters, backend="gpu", devmap=ALL_ON_GPU0, timeout=120, env_extra=dict(late, **env))
     assert r.returncode == 0 and not r.aborted, r.stderr[-2000:]
     for w in range(p):
@@ -36,18 +41,47 @@ def _run(oracle, algo, p, env, iters=3, count=1031):
 
 
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("algo,p", [("raben", 4), ("rd", 4), ("rd", 2)])
-def test_late_peer_host_gives_gate_up(oracle, algo, p):
-    r = _run(oracle, algo, p, {"FTAR_GATE_HOLD_US": "2000"})
+@pytest.mark.parametrize("algo,p,count", [("raben", 4, 1031), ("rd", 4, 1031), ("rd", 2, 1031),
+                                          ("rd", 4, (1 << 19) + 3), ("raben", 4, (1 << 19) + 3)])
+def test_late_peer_host_gives_gate_up(oracle, algo, p, count):
+    """(2 MiB: the mid-size relayed gates; the mesh's allgather is queued behind the tree,
+    whose barrier waits for the late rank's tree)"""
+    r = _run(oracle, algo, p, {"FTAR_GATE_HOLD_US": "2000", "FTAR_ONESHOT_MAX": "0" if count > 4096 else str(1 << 20)},
+             count=count)
     # call 0 allocates the workspace, whose collective absorbs the late arrival before any gate
     assert all(r.status[w][it][13] >= 1 for w in range(p - 1) for it in (1, 2)), r.status
     assert all(r.status[w][it][14] == 0 for w in range(p) for it in range(3)), r.status  # no device timeout
 
 
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("algo,p,count", [("rd", 4, (1 << 19) + 3), ("rd", 8, (1 << 21) + 5), ("raben", 4, (1 << 19) + 3),
+                                          ("raben", 8, (1 << 21) + 5), ("rd", 2, (1 << 22) - 7)])
+def test_mid_size_gates(oracle, algo, p, count):
+    """Mid-size calls (2 MiB .. 16 MiB): RD's steps 1.. and the mesh's allgather are queued
+    ahead of their barriers behind gates relayed through device memory (one workgroup polls
+    the host word), the grid capped at half the CUs so ranks sharing the GPU still run; the
+    drain before the barrier waits on a fenced marker recorded in front of the gated launch.
+    Bit-exact against the oracle (MAX over NaN / signed zeros for the operand order)."""
+    ins = H.with_specials(oracle.random_inputs(p, count, seed=p + 23), p)
+    o = oracle.rabenseifner(ins, op=2) if algo == "raben" else oracle.recursive_doubling(ins, op=2)
+    r = H.run_probe(algo, ins, op=2, iters=3, backend="gpu", devmap=ALL_ON_GPU0, timeout=200,
+                    env_extra={"FTAR_RELAY": "0", "FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0",
+                               "FTAR_GATE_TIMEOUT_MS": "10000"})
+    assert r.returncode == 0 and not r.aborted, r.stderr[-2000:]
+    per_call = (p.bit_length() - 2) if algo == "rd" else 1
+    for w in range(p):
+        for it in range(3):
+            st = r.status[w][it]
+            assert st[0] == 0 and st[10] == per_call and st[14] == 0, (w, it, st)
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+
+
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("algo,p", [("raben", 4), ("rd", 4), ("rd", 2)])
-def test_late_peer_device_gate_timeout_relaunches(oracle, algo, p):
-    r = _run(oracle, algo, p, {"FTAR_GATE_HOLD_US": "0", "FTAR_GATE_TIMEOUT_MS": "30"})
+@pytest.mark.parametrize("algo,p,count", [("raben", 4, 1031), ("rd", 4, 1031), ("rd", 2, 1031),
+                                          ("rd", 4, (1 << 19) + 3), ("raben", 4, (1 << 19) + 3)])
+def test_late_peer_device_gate_timeout_relaunches(oracle, algo, p, count):
+    r = _run(oracle, algo, p, {"FTAR_GATE_HOLD_US": "0", "FTAR_GATE_TIMEOUT_MS": "30",
+                               "FTAR_ONESHOT_MAX": "0" if count > 4096 else str(1 << 20)}, count=count)
     assert all(r.status[w][it][13] == 0 for w in range(p) for it in range(3)), r.status  # the host never gave up
     # the waiting ranks' gated launches timed out on the device and were relaunched
     assert all(r.status[w][2][14] >= 1 for w in range(p - 1)), r.status

@@ -146,7 +146,8 @@ def test_rd_repeated_calls_after_recovery(hostsim, oracle, p):
             break
     assert found, "no recovering RD kill"
     kills, o1 = found
-    r = H.run_probe("rd", inputs, kills, iters=3, backend="hostsim")
+    # (FTAR_GATE_HOLD_US=0: a loaded test host must not give gates up, the counts are checked)
+    r = H.run_probe("rd", inputs, kills, iters=3, backend="hostsim", env_extra={"FTAR_GATE_HOLD_US": "0"})
     assert not r.aborted, r.stderr[-1500:]
     order = o1.order_after
     o2 = oracle.recursive_doubling([inputs[w] for w in order])
@@ -505,7 +506,7 @@ def test_gated_launches(hostsim, oracle, algo, p, gate):
     the barriers."""
     ins = oracle.random_inputs(p, 1031, seed=p + 970)
     o = _fn(oracle, algo)(ins)
-    r = H.run_probe(algo, ins, iters=3, backend="hostsim", env_extra={"FTAR_GATE": gate})
+    r = H.run_probe(algo, ins, iters=3, backend="hostsim", env_extra={"FTAR_GATE": gate, "FTAR_GATE_HOLD_US": "0"})
     assert r.returncode == 0, r.stderr[-1000:]
     per_call = (1 if algo == "raben" else p.bit_length() - 1) if gate == "1" else 0
     for w in range(p):
@@ -514,6 +515,28 @@ def test_gated_launches(hostsim, oracle, algo, p, gate):
             assert algo == "rd" or r.status[w][it][9] == 1, r.status[w][it]
             assert r.status[w][it][10:12] == (per_call, 0), r.status[w][it]
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+
+
+@pytest.mark.parametrize("algo,p", [("rd", 2), ("rd", 4), ("rd", 8), ("raben", 4), ("raben", 8)])
+def test_gated_launches_mid_size(hostsim, oracle, algo, p):
+    """Mid-size vectors (1 MiB < S <= FTAR_GATE_MAX = 16 MiB; here 2 MiB + 12 B, read in place,
+    not staged): RD queues steps 1.. ahead of their barriers (step 0 reads the peers'
+    inputs, whose mappings are known after the first barrier only), the two-launch mesh
+    queues its allgather behind the tree; none replaced, same bits.  Above FTAR_GATE_MAX
+    nothing is gated."""
+    n = (1 << 19) + 3
+    ins = oracle.random_inputs(p, n, seed=p + 990)
+    o = _fn(oracle, algo)(ins)
+    env = {"FTAR_GATE_HOLD_US": "0", "FTAR_RELAY": "0", "FTAR_HOSTSIM_PINNED": "1"}
+    r = H.run_probe(algo, ins, iters=2, backend="hostsim", env_extra=env)
+    assert r.returncode == 0, r.stderr[-1000:]
+    per_call = (p.bit_length() - 2) if algo == "rd" else 1
+    for w in range(p):
+        for it in range(2):
+            assert r.status[w][it][10:12] == (per_call, 0), (w, it, r.status[w][it])
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+    r = H.run_probe(algo, ins, backend="hostsim", env_extra=dict(env, FTAR_GATE_MAX=str(1 << 20)))
+    assert r.returncode == 0 and all(r.status[w][0][10] == 0 for w in range(p)), r.status
 
 
 @pytest.mark.parametrize("algo", ["raben", "rd"])
@@ -525,7 +548,8 @@ def test_gated_launch_replaced_when_a_peer_reads_in_place(hostsim, oracle, algo,
     and a fresh one runs -- same bits."""
     ins = oracle.random_inputs(p, 1031, seed=p + 980)
     o = _fn(oracle, algo)(ins)
-    env = {"FTAR_PROBE_RANK_ENV": "1:FTAR_STAGE_MAX=0"}  # host entry: sbuf = the exportable staging
+    env = {"FTAR_PROBE_RANK_ENV": "1:FTAR_STAGE_MAX=0",  # host entry: sbuf = the exportable staging
+           "FTAR_GATE_HOLD_US": "0"}  # (a loaded test host must not give gates up: the counts are checked)
     r = H.run_probe(algo, ins, iters=2, backend="hostsim", env_extra=env)
     assert r.returncode == 0, r.stderr[-1000:]
     L = p.bit_length() - 1
@@ -533,10 +557,12 @@ def test_gated_launch_replaced_when_a_peer_reads_in_place(hostsim, oracle, algo,
         for it in range(2):
             st = r.status[w][it]
             assert st[0] == 0, st
-            # rank 1 stages nothing: no gate.  Raben: every other rank's one-shot reads rank
-            # 1's input -> replaced.  RD: only rank 0 reads rank 1's input (its step-0 partner)
+            # rank 1 stages nothing: no gate for its one-shot / its RD step 0 (whose operands
+            # it cannot predict), RD steps 1.. still gated (they read accumulators).  Raben:
+            # every other rank's one-shot reads rank 1's input -> replaced.  RD: only rank 0
+            # reads rank 1's input (its step-0 partner)
             if w == 1:
-                want = (0, 0)
+                want = (0, 0) if algo == "raben" else (L - 1, 0)
             elif algo == "raben":
                 want = (1, 1)
             else:

@@ -180,7 +180,7 @@ int main()
         unsigned grid = ftar::plan_segments(&in, 1, 4, 1 << 20, &L);
         L.nt_store = 1;
         const unsigned stage_tag = ++P.tag;
-        L.sig = ftar::KSignal{P.cnt, P.sig, ++P.tag, 1u, P.gate(seq), 2u * seq, P.err(), gate_ticks,
+        L.sig = ftar::KSignal{P.cnt, P.sig, ++P.tag, 1u, P.gate(seq), 2u * seq, P.err(), gate_ticks, nullptr, nullptr,
                               src, hstage, n, 4u, stage_tag, P.cnt + 16};
         CHK(ftar::launch_segments(ftar::kFloat32, ftar::kSum, L, grid, P.st));
         P.wait_flag(stage_tag);

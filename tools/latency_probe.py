@@ -4,6 +4,10 @@ the exchange kernel (hipEvents), next to a plain torch launch + synchronize issu
 every rank at once (the device round trip without the library).
 
     fault-tolerant_amd/bin/ftrun -np 2 --devmap 0,0 python tools/latency_probe.py [out.json]
+
+LAT_COUNT=<elements> (default 1024 float32 = 4 KiB) times mid-size calls, e.g. 524288 (2 MiB)
+or 2097152 (8 MiB): there RD queues steps 1.. and the mesh its allgather behind gates
+relayed through device memory (FTAR_GATE_MAX), rows *_nogate launch after the barriers.
 """
 import importlib.util
 import json
@@ -28,9 +32,11 @@ def main():
     ftar = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(ftar)
     comm = ftar.Comm.from_env()
-    x = torch.rand(1024, device="cuda")
+    count = int(os.environ.get("LAT_COUNT", "1024"))
+    iters = int(os.environ.get("LAT_ITERS", "200" if count <= 65536 else "60"))
+    x = torch.rand(count, device="cuda")
     y = torch.empty_like(x)
-    res = {"ranks": int(os.environ["FTAR_SIZE"])}
+    res = {"ranks": int(os.environ["FTAR_SIZE"]), "bytes": 4 * count}
     # plain device round trip, every rank at once
     ts = []
     for _ in range(200):
@@ -54,6 +60,7 @@ def main():
         for name, fn, limit, gate in (("raben_oneshot", comm.allreduce_rabenseifner, 1 << 20, 1),
                                       ("raben_oneshot_nogate", comm.allreduce_rabenseifner, 1 << 20, 0),
                                       ("raben_mesh", comm.allreduce_rabenseifner, 0, 1),
+                                      ("raben_mesh_nogate", comm.allreduce_rabenseifner, 0, 0),
                                       ("rd", comm.recursive_doubling, 0, 1),
                                       ("rd_nogate", comm.recursive_doubling, 0, 0)):
             comm.set_option(ftar.OPT_ONESHOT_MAX, limit)
@@ -61,7 +68,7 @@ def main():
             for _ in range(5):
                 assert fn(x, y) == 0
             wall, drain, sync, kern, cwall, gated = [], [], [], [], [], []
-            for _ in range(200):
+            for _ in range(iters):
                 comm.barrier()
                 t0 = time.perf_counter()
                 assert fn(x, y) == 0
@@ -71,7 +78,7 @@ def main():
                 sync.append(st.sync_wait_s)
                 kern.append(st.step0_kernel_ms * 1e-3)
                 cwall.append(st.wall_s)
-                gated.append(st.gated_launches)
+                gated.append(st.gated_launches - st.gated_skips)
             key = name + ("_profiled" if prof else "")
             # wall: the Python call; c_wall: inside the C entry point (ftar_stats wall_s,
             # what a C caller of include/ftar.h pays, minus the argument checks)
