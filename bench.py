@@ -1174,6 +1174,7 @@ def multi(args):
     # 1 MiB; the checks straddle it, gated and ungated, for both schedules.
     EXACT_SIZES = (("4B", 1), ("4KiB", 1024), ("64KiB", 16384), ("1MiB-16B", 262140), ("1MiB", 262144),
                    ("1MiB+16B", 262148), ("4MiB", 1 << 20))
+    MID_GATE_MAX = 16 << 20  # the mid-size gates' range the size sweep times (FTAR_OPT_GATE_MAX)
     small_fallback = {}
 
     def exact_leg():
@@ -1191,8 +1192,10 @@ def multi(args):
                 continue
             for algo, fn in (("raben", raben_fn), ("rd", rd_fn)):
                 for gate in (1, 0):
-                    small.append((f"{algo}_{label}_{'gated' if gate else 'ungated'}", base, fn, n,
-                                  {ftar.OPT_GATE: gate}))
+                    more = {ftar.OPT_GATE: gate}
+                    if gate and 4 * n > (1 << 20):  # mid-size: the relayed gates (off by default)
+                        more[ftar.OPT_GATE_MAX] = MID_GATE_MAX
+                    small.append((f"{algo}_{label}_{'gated' if gate else 'ungated'}", base, fn, n, more))
         checks += small
         if not args.no_variants:
             checks += [(name, vals, raben_fn, None, {}) for name, vals in
@@ -1207,6 +1210,7 @@ def multi(args):
             checks += [("rd_relay", (1, 1, 0, 0, 0), rd_fn, None, {}),
                        ("rd_direct", (0, 1, 0, 0, 0), rd_fn, None, {})]
         gate0 = comm.get_option(ftar.OPT_GATE)
+        gmax0 = comm.get_option(ftar.OPT_GATE_MAX)
         flag0 = comm.get_option(ftar.OPT_FLAG_SYNC)
 
         def run(cks, extra=None):
@@ -1220,6 +1224,7 @@ def multi(args):
                 maybe_fail(f"exact:{name}")
                 fails.append(exact_ok(fn, n=n))
                 comm.set_option(ftar.OPT_GATE, gate0)
+                comm.set_option(ftar.OPT_GATE_MAX, gmax0)
             return max_over_ranks(fails) if fails else []
 
         comm.set_profiling(False)
@@ -1342,6 +1347,7 @@ def multi(args):
                  "gate": comm.get_option(ftar.OPT_GATE), "flag_sync": comm.get_option(ftar.OPT_FLAG_SYNC)}
         comm.set_profiling(False)  # no kernel events: the plain per-call cost
         oneshot_max = comm.get_option(ftar.OPT_ONESHOT_MAX)
+        gate_max0 = comm.get_option(ftar.OPT_GATE_MAX)
         z = x.clone() if nccl else None
         n = 1
         try:
@@ -1354,14 +1360,22 @@ def multi(args):
                 # time in one-GPU rehearsals, profiles/r03/README.md)
                 steps, warm = (100, 50) if 4 * n <= (1 << 20) else (20, 3) if n <= (1 << 22) else (5, 2)
                 row = {"bytes": 4 * n}
+                mid = gate_max0 < 4 * n <= MID_GATE_MAX and comm.get_option(ftar.OPT_GATE) != 0
                 for name, fn, extra in (("raben", comm.allreduce_rabenseifner, None),
-                                        ("raben_no_oneshot", comm.allreduce_rabenseifner, 0),
-                                        ("rd", comm.recursive_doubling, None)):
-                    if extra is not None:
-                        if not (pow2 and comm.get_option(ftar.OPT_MESH) and oneshot_max > 0) or \
-                                (world > 2 and 4 * n > oneshot_max):
-                            continue
-                        comm.set_option(ftar.OPT_ONESHOT_MAX, extra)
+                                        ("raben_no_oneshot", comm.allreduce_rabenseifner, {ftar.OPT_ONESHOT_MAX: 0}),
+                                        ("rd", comm.recursive_doubling, None),
+                                        # mid-size calls with their predictable launches queued
+                                        # behind relayed gates (off by default: DESIGN.md 6)
+                                        ("raben_midgate", comm.allreduce_rabenseifner,
+                                         {ftar.OPT_GATE_MAX: MID_GATE_MAX}),
+                                        ("rd_midgate", comm.recursive_doubling, {ftar.OPT_GATE_MAX: MID_GATE_MAX})):
+                    if name == "raben_no_oneshot" and (not (pow2 and comm.get_option(ftar.OPT_MESH) and oneshot_max > 0)
+                                                       or (world > 2 and 4 * n > oneshot_max)):
+                        continue
+                    if name.endswith("_midgate") and not mid:
+                        continue
+                    for o, v in (extra or {}).items():
+                        comm.set_option(o, v)
 
                     def call(fn=fn, n=n):
                         if fn(x, y, count=n) != 0:
@@ -1376,6 +1390,7 @@ def multi(args):
                                 "gated_launches": comm.last_stats().gated_launches}
                     finally:
                         comm.set_option(ftar.OPT_ONESHOT_MAX, oneshot_max)
+                        comm.set_option(ftar.OPT_GATE_MAX, gate_max0)
                 if z is not None:
                     zn = z[:n]
                     row["rccl_us"] = round(quick(lambda: dist.all_reduce(zn), steps=steps, warmup=warm) * 1e6, 2)

@@ -31,6 +31,7 @@ OPT_PUSH = 8
 OPT_GATE = 9
 OPT_FLAG_SYNC = 10
 OPT_TREE_UNROLL = 11
+OPT_GATE_MAX = 12
 REDUNDANCY_NEVER, REDUNDANCY_ALWAYS, REDUNDANCY_AUTO = 0, 1, 2  # OPT_REDUNDANCY values
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
 ERR_OP = 9  # MPI_ERR_OP: a logical / bitwise op on a float type

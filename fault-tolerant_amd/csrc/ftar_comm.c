@@ -161,7 +161,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->push = getenv("FTAR_PUSH") ? atoi(getenv("FTAR_PUSH")) : 0;
     c->gate = getenv("FTAR_GATE") ? atoi(getenv("FTAR_GATE")) != 0 : 1;
     c->gate_hold_s = (getenv("FTAR_GATE_HOLD_US") ? atof(getenv("FTAR_GATE_HOLD_US")) : 2000.0) * 1e-6;
-    c->gate_max = getenv("FTAR_GATE_MAX") ? (size_t)atoll(getenv("FTAR_GATE_MAX")) : ((size_t)16 << 20);
+    c->gate_max = getenv("FTAR_GATE_MAX") ? (size_t)atoll(getenv("FTAR_GATE_MAX")) : ((size_t)1 << 20);
     c->oneshot_max = getenv("FTAR_ONESHOT_MAX") ? (size_t)atoll(getenv("FTAR_ONESHOT_MAX")) : ((size_t)1 << 20);
     c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
     c->stage_max = getenv("FTAR_STAGE_MAX") ? (size_t)atoll(getenv("FTAR_STAGE_MAX")) : ((size_t)1 << 20);
@@ -443,6 +443,7 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_ONESHOT_MAX: c->oneshot_max = (size_t)v; break;
     case FTAR_OPT_PUSH: c->push = v >= 2 ? 2 : v != 0; break;
     case FTAR_OPT_GATE: c->gate = v != 0; break;
+    case FTAR_OPT_GATE_MAX: c->gate_max = (size_t)v; break;
     case FTAR_OPT_FLAG_SYNC:
         if (fdev_set_knob(c->dev, FDEV_KNOB_FLAG_SYNC, v != 0)) return FTAR_ERR_ARG;
         break;
@@ -468,6 +469,7 @@ int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
     case FTAR_OPT_ONESHOT_MAX: *v = (double)c->oneshot_max; break;
     case FTAR_OPT_PUSH: *v = c->push; break;
     case FTAR_OPT_GATE: *v = c->gate; break;
+    case FTAR_OPT_GATE_MAX: *v = (double)c->gate_max; break;
     case FTAR_OPT_FLAG_SYNC: *v = fdev_get_knob(c->dev, FDEV_KNOB_FLAG_SYNC); break;
     case FTAR_OPT_TREE_UNROLL: *v = fdev_get_knob(c->dev, FDEV_KNOB_TREE_UNROLL); break;
     default: return FTAR_ERR_ARG;

@@ -88,7 +88,7 @@ struct ftar_comm {
     int push;            /* FTAR_PUSH (default 0): the mesh by remote stores -- 1 reduce-scatter, 2 both phases */
     int gate;            /* FTAR_GATE (default 1): small exchange launches queued ahead of their barrier, gated */
     double gate_hold_s;  /* FTAR_GATE_HOLD_US: a barrier waiting longer gives the pending gated launch up (0 = never) */
-    size_t gate_max;     /* FTAR_GATE_MAX bytes (default 16 MiB): largest vector whose launches are queued ahead */
+    size_t gate_max;     /* FTAR_GATE_MAX bytes (default 1 MiB): largest vector whose launches are queued ahead */
     size_t oneshot_max;  /* FTAR_ONESHOT_MAX bytes: mesh Raben in one launch up to this size */
     double loop_seconds; /* FTAR_LOOP_SECONDS: stretch the tolerant step loop to this long (harness knob) */
     /* the step's last peer read (FTAR_LOOP_SECONDS re-pulls it into pad while it waits) */

@@ -219,9 +219,14 @@ typedef enum {
     FTAR_OPT_FLAG_SYNC = 10,   /* short launches (<= 64 workgroups) signal their own completion through
                                   a pinned host word instead of a fenced marker drain (0/1, default 1;
                                   0 also turns the gates off) */
-    FTAR_OPT_TREE_UNROLL = 11  /* 16-byte vectors per lane and source in the mesh's tree kernel at
+    FTAR_OPT_TREE_UNROLL = 11, /* 16-byte vectors per lane and source in the mesh's tree kernel at
                                   p = 4, 8 (1, 2 or 4; default 1): more loads in flight per lane for
                                   remote (xGMI) sources; same bits */
+    FTAR_OPT_GATE_MAX = 12     /* largest vector, in bytes, whose predictable launches are queued ahead
+                                  behind gates (default 1 MiB).  Above 1 MiB (mid-size: RD steps 1..,
+                                  the mesh's allgather) the gate is relayed through device memory and
+                                  the launch waits on up to half the CUs -- slower on a GPU shared by
+                                  several ranks, so bench.py times it on the node */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);

@@ -54,9 +54,14 @@ def test_library_loads_and_binds(built):
     assert b"gfx950" in L.ftar_version()
 
 
-def test_kernels_are_gfx950_code_objects(built):
-    """The HIP kernels are compiled for gfx950 and nothing else (no CUDA/dual path)."""
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", built], capture_output=True,
+def test_kernels_are_gfx950_code_objects(built, tmp_path):
+    """The HIP kernels are compiled for gfx950 and nothing else (no CUDA/dual path).
+    (llvm-objdump --offloading extracts the images next to its input: a copy in tmp_path,
+    so nothing lands in lib/.)"""
+    import shutil
+    copy = str(tmp_path / "libftar.so")
+    shutil.copy(built, copy)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", copy], capture_output=True,
                          text=True).stdout
     assert "gfx950" in out
     for other in ("gfx90a", "gfx942", "sm_"):

@@ -30,7 +30,7 @@ def _run(oracle, algo, p, env, iters=3, count=1031):
     # (FTAR_LOOP_SECONDS: the barriers of steps 1.. / the reduce-scatter's agree, behind which
     # the next launch is gated)
     late = {"FTAR_PROBE_RANK_ENV": f"{p - 1}:FTAR_PROBE_SLEEP_US=300000" if count <= 4096 else
-            f"{p - 1}:FTAR_LOOP_SECONDS=0.3", "FTAR_RELAY": "0", "FTAR_HOST_PIPE": "0"}
+            f"{p - 1}:FTAR_LOOP_SECONDS=0.3", "FTAR_RELAY": "0", "FTAR_HOST_PIPE": "0", "FTAR_GATE_MAX": str(16 << 20)}
     r = H.run_probe(algo, ins, iters=iters, backend="gpu", devmap=ALL_ON_GPU0, timeout=120, env_extra=dict(late, **env))
     assert r.returncode == 0 and not r.aborted, r.stderr[-2000:]
     for w in range(p):
@@ -57,7 +57,8 @@ def test_late_peer_host_gives_gate_up(oracle, algo, p, count):
 @pytest.mark.parametrize("algo,p,count", [("rd", 4, (1 << 19) + 3), ("rd", 8, (1 << 21) + 5), ("raben", 4, (1 << 19) + 3),
                                           ("raben", 8, (1 << 21) + 5), ("rd", 2, (1 << 22) - 7)])
 def test_mid_size_gates(oracle, algo, p, count):
-    """Mid-size calls (2 MiB .. 16 MiB): RD's steps 1.. and the mesh's allgather are queued
+    """Mid-size calls (2 MiB .. 16 MiB, FTAR_GATE_MAX = 16 MiB; off by default):
+    RD's steps 1.. and the mesh's allgather are queued
     ahead of their barriers behind gates relayed through device memory (one workgroup polls
     the host word), the grid capped at half the CUs so ranks sharing the GPU still run; the
     drain before the barrier waits on a fenced marker recorded in front of the gated launch.
@@ -66,7 +67,7 @@ def test_mid_size_gates(oracle, algo, p, count):
     o = oracle.rabenseifner(ins, op=2) if algo == "raben" else oracle.recursive_doubling(ins, op=2)
     r = H.run_probe(algo, ins, op=2, iters=3, backend="gpu", devmap=ALL_ON_GPU0, timeout=200,
                     env_extra={"FTAR_RELAY": "0", "FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0",
-                               "FTAR_GATE_TIMEOUT_MS": "10000"})
+                               "FTAR_GATE_TIMEOUT_MS": "10000", "FTAR_GATE_MAX": str(16 << 20)})
     assert r.returncode == 0 and not r.aborted, r.stderr[-2000:]
     per_call = (p.bit_length() - 2) if algo == "rd" else 1
     for w in range(p):

@@ -519,15 +519,15 @@ def test_gated_launches(hostsim, oracle, algo, p, gate):
 
 @pytest.mark.parametrize("algo,p", [("rd", 2), ("rd", 4), ("rd", 8), ("raben", 4), ("raben", 8)])
 def test_gated_launches_mid_size(hostsim, oracle, algo, p):
-    """Mid-size vectors (1 MiB < S <= FTAR_GATE_MAX = 16 MiB; here 2 MiB + 12 B, read in place,
-    not staged): RD queues steps 1.. ahead of their barriers (step 0 reads the peers'
+    """Mid-size vectors (1 MiB < S <= FTAR_GATE_MAX, set to 16 MiB -- the default is 1 MiB, see
+    DESIGN.md 6; here 2 MiB + 12 B, read in place, not staged): RD queues steps 1.. ahead of their barriers (step 0 reads the peers'
     inputs, whose mappings are known after the first barrier only), the two-launch mesh
     queues its allgather behind the tree; none replaced, same bits.  Above FTAR_GATE_MAX
     nothing is gated."""
     n = (1 << 19) + 3
     ins = oracle.random_inputs(p, n, seed=p + 990)
     o = _fn(oracle, algo)(ins)
-    env = {"FTAR_GATE_HOLD_US": "0", "FTAR_RELAY": "0", "FTAR_HOSTSIM_PINNED": "1"}
+    env = {"FTAR_GATE_HOLD_US": "0", "FTAR_RELAY": "0", "FTAR_HOSTSIM_PINNED": "1", "FTAR_GATE_MAX": str(16 << 20)}
     r = H.run_probe(algo, ins, iters=2, backend="hostsim", env_extra=env)
     assert r.returncode == 0, r.stderr[-1000:]
     per_call = (p.bit_length() - 2) if algo == "rd" else 1

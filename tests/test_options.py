@@ -36,8 +36,9 @@ def test_option_defaults_and_roundtrip(solo):
     assert [_get(L, h, o) for o in range(6)] == [1.0, 1.0, float(4 << 20), 0.0, 0.0, 2.0]
     # flag-signalled drains on, tree kernel one vector per lane and source
     assert _get(L, h, 10) == 1.0 and _get(L, h, 11) == 1.0
+    assert _get(L, h, 12) == float(1 << 20)  # mid-size gates off by default
     for opt, val in ((0, 0), (1, 0), (2, 1 << 20), (3, 0.5), (4, 1), (5, 1), (5, 0), (5, 2), (10, 0), (10, 1),
-                     (11, 2), (11, 4), (11, 1)):
+                     (11, 2), (11, 4), (11, 1), (12, 16 << 20), (12, 0)):
         assert L.ftar_comm_set_option(h, opt, val) == 0
         assert _get(L, h, opt) == val
 
