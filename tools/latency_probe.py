@@ -65,6 +65,8 @@ def main():
                                       ("rd_nogate", comm.recursive_doubling, 0, 0)):
             comm.set_option(ftar.OPT_ONESHOT_MAX, limit)
             comm.set_option(ftar.OPT_GATE, gate)
+            # mid-size gates are off by default (FTAR_OPT_GATE_MAX = 1 MiB): on for the gated rows
+            comm.set_option(ftar.OPT_GATE_MAX, 16 << 20 if gate else 1 << 20)
             for _ in range(5):
                 assert fn(x, y) == 0
             wall, drain, sync, kern, cwall, gated = [], [], [], [], [], []
