@@ -376,6 +376,8 @@ def c5_leg(world, devices, count, ranks, deadline, calls=6, kill_call=2):
             # the reference's corr path); later calls sum the survivors'
             want = want_all - (victim if (kill and c > kill_call) else 0)
             per_call.append({"ms_max_over_ranks": round(max(p["ms"] for p in per), 3) if per else None,
+                             # algorithmic local HBM bytes of the busiest rank's kernels (ftar_stats.hbm_bytes)
+                             "hbm_bytes_max_over_ranks": max((p.get("hbm_bytes", 0) for p in per), default=None),
                              "recoveries": max((p["recoveries"] for p in per), default=None),
                              "comm_size_after": min((p["comm_size"] for p in per), default=None),
                              "result_ok": bool(per) and all(p["rc"] == 0 and p["uniform"] and p["value"] == want
@@ -412,6 +414,7 @@ def c5_leg(world, devices, count, ranks, deadline, calls=6, kill_call=2):
             s["recovered_call_ms"] = fc[kill_call]["ms_max_over_ranks"]
             s["recovered_ag_call_ms"] = fa["calls"][kill_call]["ms_max_over_ranks"]
             s["no_fault_call_ms"] = med(n["calls"][1:])  # median after the warm-up call
+            s["no_fault_hbm_bytes"] = n["calls"][-1].get("hbm_bytes_max_over_ranks")
             s["recovery_overhead_ms"] = round(s["recovered_call_ms"] - s["no_fault_call_ms"], 3)
             s["pre_fault_call_ms"] = med(fc[1:kill_call])
             s["survivors_call_ms"] = med(fc[kill_call + 1:])  # p - 1 ranks after the shrink

@@ -69,7 +69,7 @@ int main(int argc, char **argv)
     CHECK_HIP(hipMemcpy(s, h, count * sizeof(float), hipMemcpyHostToDevice));
     CHECK_HIP(hipDeviceSynchronize());
 
-    double ms[MAX_CALLS], value[MAX_CALLS];
+    double ms[MAX_CALLS], value[MAX_CALLS], hbm[MAX_CALLS];
     int rc[MAX_CALLS], rec[MAX_CALLS], size_after[MAX_CALLS], uniform[MAX_CALLS], step0_copy = 0;
     for (int c = 0; c < calls; c++) {
         rc[c] = rd ? ftar_recursive_doubling(s, r, count, FTAR_FLOAT32, FTAR_SUM, comm)
@@ -77,6 +77,7 @@ int main(int argc, char **argv)
         ftar_stats st;
         ftar_last_stats(comm, &st);
         ms[c] = st.wall_s * 1e3;
+        hbm[c] = st.hbm_bytes; /* algorithmic local HBM bytes of this rank's kernels */
         rec[c] = st.recoveries;
         size_after[c] = st.comm_size_after;
         step0_copy |= st.step0_copy;
@@ -101,8 +102,9 @@ int main(int argc, char **argv)
     printf("{\"rank\": %d, \"size\": %d, \"device\": %d, \"step0_copy\": %d, \"calls\": [", wrank, wsize, dev,
            step0_copy);
     for (int c = 0; c < calls; c++)
-        printf("%s{\"rc\": %d, \"ms\": %.4f, \"recoveries\": %d, \"comm_size\": %d, \"value\": %.1f, \"uniform\": %s}",
-               c ? ", " : "", rc[c], ms[c], rec[c], size_after[c], value[c], uniform[c] ? "true" : "false");
+        printf("%s{\"rc\": %d, \"ms\": %.4f, \"recoveries\": %d, \"comm_size\": %d, \"value\": %.1f, \"uniform\": %s, "
+               "\"hbm_bytes\": %.0f}",
+               c ? ", " : "", rc[c], ms[c], rec[c], size_after[c], value[c], uniform[c] ? "true" : "false", hbm[c]);
     printf("]}\n");
     fflush(stdout);
     ftar_finalize(comm);
