@@ -134,8 +134,6 @@ struct ftar_dev {
     // that timed out (or was found overtaken) is reported in sig_flag[32].
     unsigned gate_seq;     // sequence of the last gate (the word's value = 2 x seq, + 1 = skip)
     int gate_pending;      // queued, gate still closed
-    int gate_verify;       // opened: check gate verify_seq's timeout word at the next drain
-    unsigned verify_seq;
     int pre_gate_any;      // signalled launches queued before the gated one since the last drain ...
     unsigned pre_gate_tag; // ... the last of them
     unsigned long long gate_ticks; // wall-clock ticks before a closed gate counts as timed out
@@ -147,6 +145,7 @@ struct ftar_dev {
     // (gated launches never write what they read, so running a part of one twice is harmless).
     struct GatedPlan {
         int valid, batch, dtype, op, nsrc;
+        int opened; // opened as go: check its timeout word once it has completed (verify_gate)
         unsigned grid, seq;
         ftar::KSegList L;
         ftar::TreeBatch B;
@@ -208,8 +207,7 @@ int fdev_open(int device, ftar_dev **out)
         d->sig_tag = 0;
         d->unsignalled = d->signalled = d->need_acquire = d->force_fence = 0;
         d->gate_seq = 0;
-        d->gate_pending = d->gate_verify = d->pre_gate_any = 0;
-        d->verify_seq = 0;
+        d->gate_pending = d->pre_gate_any = 0;
         d->user_host_waits = 0;
         d->pre_gate_tag = 0;
         d->gate_relaunches = 0;
@@ -659,6 +657,7 @@ static void keep_plan(ftar_dev *d, int batch, int dtype, int op, int nsrc, unsig
 {
     ftar_dev::GatedPlan &g = d->gp[d->gate_seq & 1];
     g.valid = 1;
+    g.opened = 0;
     g.batch = batch;
     g.dtype = dtype;
     g.op = op;
@@ -764,8 +763,13 @@ int fdev_gate_open(ftar_dev *d, int skip)
     }
     d->gate_pending = 0;
     d->big_pending = 0;
-    d->gate_verify = 1;
-    d->verify_seq = d->gate_seq;
+    // a launch opened as go is checked at the drain that completes it (verify_gate); one given
+    // up needs no check: its step launches normally, and the kept plan must never run after it
+    ftar_dev::GatedPlan &g = d->gp[d->gate_seq & 1];
+    if (g.valid && g.seq == d->gate_seq) {
+        if (skip) g.valid = 0;
+        else g.opened = 1;
+    }
     return 0;
 }
 
@@ -1036,39 +1040,39 @@ static int wait_signal(ftar_dev *d, unsigned tag, int (*poll)(void *), void *arg
     }
 }
 
-// The opened gate d->verify_seq has completed: did the device give it up (its gate stayed
-// closed past the timeout, or a late workgroup found the slot overtaken)?  Then its
-// workgroups (some or all) returned without touching memory, and the plan runs again
-// ungated -- after a fenced marker (device-wide acquire: the peers' current data) and
-// drained through one (release: visible to the peers before this rank arrives anywhere).
-// Any launch pending behind its own gate is given up first (nothing waits behind a closed
-// gate); its step then launches normally.
+// The gates opened as go have completed (every drain covers the launches queued before any
+// still-pending gate): did the device give one up (its gate stayed closed past the timeout,
+// or a late workgroup found the slot overtaken)?  Then its workgroups (some or all) returned
+// without touching memory, and the plan runs again ungated -- after a fenced marker
+// (device-wide acquire: the peers' current data) and drained through one (release: visible
+// to the peers before this rank arrives anywhere).  Any launch pending behind its own gate is
+// given up first (nothing waits behind a closed gate); its step then launches normally.
 static int verify_gate(ftar_dev *d, int (*poll)(void *), void *arg)
 {
-    if (!d->gate_verify) return 0;
-    d->gate_verify = 0;
-    const unsigned seq = d->verify_seq;
-    unsigned *err = gate_err(d, seq);
-    if (__atomic_load_n(err, __ATOMIC_ACQUIRE) != 2u * seq) return 0;
-    __atomic_store_n(err, 0u, __ATOMIC_RELAXED);
-    ftar_dev::GatedPlan &g = d->gp[seq & 1];
-    if (!g.valid || g.seq != seq) {
-        snprintf(g_err, sizeof(g_err), "gated launch %u: its gate timed out and its plan is gone", seq);
-        return 101;
+    int redo = 0;
+    for (unsigned k = 0; k < 2; k++) {
+        // the older of the two first, and a later one again after a relaunch (it may have
+        // read what the given-up one should have written): the steps' order is kept
+        ftar_dev::GatedPlan &g = d->gp[(d->gate_seq + 1 + k) & 1];
+        if (!g.valid || !g.opened) continue;
+        g.valid = 0;
+        unsigned *err = gate_err(d, g.seq);
+        if (__atomic_load_n(err, __ATOMIC_ACQUIRE) != 2u * g.seq && !redo) continue;
+        __atomic_store_n(err, 0u, __ATOMIC_RELAXED);
+        if (d->gate_pending) (void)fdev_gate_open(d, 1);
+        fprintf(stderr, "ftar: device %d: gated launch %u %s: relaunched\n", d->device, g.seq,
+                redo++ ? "ran after a relaunched one" : "was given up by the device (gate timeout)");
+        HIPCHK(hipEventRecord(d->fence_main, d->stream));
+        hipError_t e = g.batch ? ftar::launch_tree_batch(g.dtype, g.op, g.nsrc, g.B, g.grid, d->stream)
+                               : ftar::launch_segments(g.dtype, g.op, g.L, g.grid, d->stream);
+        if (e != hipSuccess) return set_err(e, "relaunch of a timed-out gated launch");
+        d->gate_relaunches++;
+        int rc = sync_stream(d, d->stream, poll, arg);
+        d->need_acquire = 0;
+        d->unsignalled = d->signalled = d->force_fence = 0;
+        if (rc) return rc;
     }
-    if (d->gate_pending) (void)fdev_gate_open(d, 1);
-    fprintf(stderr, "ftar: device %d: gated launch %u was given up by the device (gate timeout): relaunched\n",
-            d->device, seq);
-    HIPCHK(hipEventRecord(d->fence_main, d->stream));
-    hipError_t e = g.batch ? ftar::launch_tree_batch(g.dtype, g.op, g.nsrc, g.B, g.grid, d->stream)
-                           : ftar::launch_segments(g.dtype, g.op, g.L, g.grid, d->stream);
-    if (e != hipSuccess) return set_err(e, "relaunch of a timed-out gated launch");
-    g.valid = 0;
-    d->gate_relaunches++;
-    int rc = sync_stream(d, d->stream, poll, arg);
-    d->need_acquire = 0;
-    d->unsignalled = d->signalled = d->force_fence = 0;
-    return rc;
+    return 0;
 }
 
 static int spin(hipEvent_t e, int (*poll)(void *), void *arg);

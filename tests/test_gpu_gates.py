@@ -87,3 +87,16 @@ def test_late_peer_device_gate_timeout_relaunches(oracle, algo, p, count):
     # the waiting ranks' gated launches timed out on the device and were relaunched
     assert all(r.status[w][2][14] >= 1 for w in range(p - 1)), r.status
     assert "relaunched" in r.stderr, r.stderr[-1500:]
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("algo,p,count", [("raben", 4, 1031), ("rd", 4, 1031), ("rd", 4, (1 << 19) + 3)])
+def test_device_timeout_then_host_hold_never_relaunches(oracle, algo, p, count):
+    """The device gives the gate up first (30 ms), then the host's hold (100 ms) gives the
+    launch up as well and the step launches after the barrier: the kept plan must not run
+    again at the next drain (it could be stale by then, e.g. after a recovery)."""
+    r = _run(oracle, algo, p, {"FTAR_GATE_HOLD_US": "100000", "FTAR_GATE_TIMEOUT_MS": "30",
+                               "FTAR_ONESHOT_MAX": "0" if count > 4096 else str(1 << 20)}, count=count)
+    assert all(r.status[w][it][13] >= 1 for w in range(p - 1) for it in (1, 2)), r.status
+    assert all(r.status[w][it][14] == 0 for w in range(p) for it in range(3)), r.status
+    assert "relaunched" not in r.stderr, r.stderr[-1500:]
