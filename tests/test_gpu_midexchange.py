@@ -164,14 +164,21 @@ def _seeds(var, default):
     return [int(t) for t in v.split(",")]
 
 
+KILL_COUNTS = [int(c) for c in os.environ.get("FTAR_GPU_KILL_COUNTS", "").split(",") if c]
+
+
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("seed", _seeds("FTAR_GPU_KILL_SEEDS", [0, 1]))
-def test_random_kill_points_gpu(oracle, seed):
+@pytest.mark.parametrize("seed,count", [(s, c) for s in _seeds("FTAR_GPU_KILL_SEEDS", [0, 1])
+                                        for c in (KILL_COUNTS or [(1 << 20) + 3])] +
+                         ([] if KILL_COUNTS else [(0, 1031)]))
+def test_random_kill_points_gpu(oracle, seed, count):
     """Random single kills (any victim, phase, step and point -- DURING weighted up) on
-    the GPU, p = 5 / 9 (one idle spare) and 6 / 8, both schedules, 1 Mi elements, MAX over
-    NaN / signed zeros so the recovery path shows in the bits: outcome class and every
-    survivor's result as the oracle's.  Twelve jobs per seed, each a real process
-    teardown, most with a peer's kernel reading the victim's HBM."""
+    the GPU, p = 5 / 9 (one idle spare) and 6 / 8, both schedules, 1 Mi elements (and 1031:
+    the small calls, whose launches wait behind gates -- a victim may die with its gated
+    launch queued), MAX over NaN / signed zeros so the recovery path shows in the bits:
+    outcome class and every survivor's result as the oracle's.  Twelve jobs per seed, each a
+    real process teardown, most with a peer's kernel reading the victim's HBM.
+    FTAR_GPU_KILL_COUNTS ("1031,65536") sets the lengths of a one-off campaign."""
     import random
     rng = random.Random(seed)
     n = 0
@@ -181,7 +188,7 @@ def test_random_kill_points_gpu(oracle, seed):
         kill = (rng.randrange(p), rng.choice([1, 2]) if algo == "raben" else 1, rng.randrange(3),
                 rng.choice([3, 3, 0, 1, 2]))
         fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
-        ins = H.with_specials(oracle.random_inputs(p, (1 << 20) + 3, seed=seed * 100 + n), p)
+        ins = H.with_specials(oracle.random_inputs(p, count, seed=seed * 100 + n), p)
         if fn(ins, [kill], op=2).status[kill[0]] != oracle.DEAD:
             continue  # the schedule never reaches this point (e.g. a step it does not have)
         _check(fn, algo, ins, [kill], op=2)

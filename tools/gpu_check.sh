@@ -4,7 +4,8 @@
 #   STEPS=smoke,pytest,bench,prof,pmc bash tools/gpu_check.sh
 # Steps (comma list):
 #   smoke      __graft_entry__.smoke()
-#   pytest     the whole -m gpu suite (heartbeat file under $OUT for long cases)
+#   pytest     the whole -m gpu suite (heartbeat file under $OUT for long cases); PYTEST_PATHS
+#              narrows it (test ids, space-separated), PYTEST_ARGS adds options (no spaces inside one)
 #   bench      bench.py N = 1 (rotating buffers) and its register-kernel variant
 #   prof       rocprofv3 kernel trace + stats of bench.py N = 1
 #   pmc        one rocprofv3 --pmc pass per counter (FETCH_SIZE, WRITE_SIZE) of bench.py
@@ -38,7 +39,7 @@ if has smoke; then
   rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; [ $rc -eq 0 ] || exit $rc
 fi
 if has pytest; then
-  FTAR_HEARTBEAT=$OUT/heartbeat.txt timeout -k 10 ${PYTEST_TIMEOUT:-1500} python -u -m pytest tests -m gpu -v \
+  FTAR_HEARTBEAT=$OUT/heartbeat.txt timeout -k 10 ${PYTEST_TIMEOUT:-1500} python -u -m pytest ${PYTEST_PATHS:-tests} -m gpu -v \
       --timeout 900 --timeout-method thread -p no:cacheprovider -rf --durations=25 ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; tail -6 "$OUT/pytest_gpu.log"; stop_on_fault $rc pytest
 fi
