@@ -6,6 +6,8 @@
 # reference's policy (R-state processes named main) restricted to this job's processes,
 # so nothing else on the machine can be hit.
 #   tools/fault_campaign.sh OUTDIR [RUNS]
+# FTAR_CAMPAIGN_ALGOS ("raben rd") and FTAR_CAMPAIGN_KILLS ("0 1") narrow it, e.g. the
+# reference's configs[4] shape: FTAR_NMIN=9 FTAR_NMAX=9 FTAR_CAMPAIGN_ALGOS=raben FTAR_CAMPAIGN_KILLS=1.
 # Writes OUTDIR/log_{nokill,single}_{RD,Raben}.csv (check_fault.py rows), one progress
 # line per run on stdout.
 set -u
@@ -17,9 +19,9 @@ export FTAR_KILLER=$ROOT/tests/scoped_kill.sh
 export FTAR_NMIN=${FTAR_NMIN:-5} FTAR_NMAX=${FTAR_NMAX:-8}
 EXEDIR=${FTAR_EXE_DIR:-../src}  # relative to run/ (run_mpi.sh starts ./$EXE)
 cd "$ROOT/fault-tolerant_amd/run"
-for algo in raben rd; do
+for algo in ${FTAR_CAMPAIGN_ALGOS:-raben rd}; do
     tag=$([ $algo = raben ] && echo Raben || echo RD)
-    for kill in 0 1; do
+    for kill in ${FTAR_CAMPAIGN_KILLS:-0 1}; do
         name=$([ $kill = 0 ] && echo nokill || echo single)
         for ((i = 0; i < RUNS; i++)); do
             ./run_test.sh $kill "$OUT/log_${name}_${tag}.csv" $algo $EXEDIR/$algo/main > /dev/null 2>&1
