@@ -131,7 +131,7 @@ struct ftar_dev {
     int force_fence;       // the next drain must be a fenced marker (peers read caller memory in place)
     // A launch queued ahead of its barrier (fdev_tree_batch_gated / fdev_run_gated): its
     // workgroups wait on a gate word (sig_flag[16 + seq % 8]) until fdev_gate_open; a gate
-    // that timed out (or was found overtaken) is reported in sig_flag[32].
+    // that timed out (or was found overtaken) is reported in its slot's word sig_flag[32 + seq % 8].
     unsigned gate_seq;     // sequence of the last gate (the word's value = 2 x seq, + 1 = skip)
     int gate_pending;      // queued, gate still closed
     int pre_gate_any;      // signalled launches queued before the gated one since the last drain ...
