@@ -79,6 +79,54 @@ __global__ __launch_bounds__(256) void k_lds(v4f *__restrict__ io, const v4f *__
     for (int u = 0; u < U; u++) st<NTS>(io + base + u * 256 + threadIdx.x, a[u] + stage[u * 256 + threadIdx.x]);
 }
 
+// both operands staged HBM -> LDS by the DMA path (no VGPR loads at all); stores as k_lds
+template <int U, int AUX, int NTS>
+__global__ __launch_bounds__(256) void k_lds2(v4f *__restrict__ io, const v4f *__restrict__ in, size_t nv)
+{
+    __shared__ v4f sa[U * 256], sb[U * 256];
+    const int wave = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * U * 256;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(io + base + u * 256 + threadIdx.x),
+                                         (__attribute__((address_space(3))) void *)&sa[u * 256 + wave * 64], 16, 0, AUX);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(in + base + u * 256 + threadIdx.x),
+                                         (__attribute__((address_space(3))) void *)&sb[u * 256 + wave * 64], 16, 0, AUX);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++) st<NTS>(io + base + u * 256 + threadIdx.x, sa[u * 256 + threadIdx.x] + sb[u * 256 + threadIdx.x]);
+}
+
+// the product's LDS-DMA kernel with the 16-byte stores' cache policy set explicitly
+// (POL: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1, 4 sc0 sc1 nt, 5 sc1 nt)
+template <int POL> __device__ __forceinline__ void stp(v4f *p, v4f v)
+{
+    if constexpr (POL == 0) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+template <int U, int POL>
+__global__ __launch_bounds__(256) void k_ldsp(v4f *__restrict__ io, const v4f *__restrict__ in, size_t nv)
+{
+    __shared__ v4f stage[U * 256];
+    const int wave = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * U * 256;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(in + base + u * 256 + threadIdx.x),
+                                         (__attribute__((address_space(3))) void *)&stage[u * 256 + wave * 64], 16, 0, 2);
+    v4f a[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) a[u] = ld<1>(io + base + u * 256 + threadIdx.x);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++) stp<POL>(io + base + u * 256 + threadIdx.x, a[u] + stage[u * 256 + threadIdx.x]);
+}
+
 // persistent grid-stride with a software pipeline: the next tile's loads are issued
 // before the current tile's stores
 template <int U, int NTL, int NTS = 0>
@@ -225,6 +273,29 @@ int main(int argc, char **argv)
                 snprintf(nm, sizeof(nm), "pipe U2 ntl1 nts1 grid%d", G);
                 run(nm, B3, true, [&](int r) { k_pipe<2, 1, 1><<<G, 256>>>(io[r], in[r], nv); });
             }
+        }
+        printf("BEST %s %.1f us %.1f GB/s\n", best, best_us, B3 / (best_us * 1e-6) / 1e9);
+        return 0;
+    }
+    if (argc > 3 && argv[3][0] == 'x') { // both operands by LDS DMA; explicit store policies
+        for (int rep = 0; rep < 3; rep++) {
+            LDSS(4, 0, 2, 1) // the product's kernel
+#define LDS2(U, AUX, NS)                                                                                    \
+    snprintf(nm, sizeof(nm), "lds2 U%d aux%d nts%d", U, AUX, NS);                                          \
+    run(nm, B3, true, [&](int r) { k_lds2<U, AUX, NS><<<(unsigned)(nv / (U * 256)), 256>>>(io[r], in[r], nv); });
+#define LDSP(U, POL)                                                                                        \
+    snprintf(nm, sizeof(nm), "lds U%d store-policy %d", U, POL);                                           \
+    run(nm, B3, true, [&](int r) { k_ldsp<U, POL><<<(unsigned)(nv / (U * 256)), 256>>>(io[r], in[r], nv); });
+            LDS2(2, 2, 1)
+            LDS2(4, 2, 1)
+            LDS2(4, 0, 1)
+            LDS2(8, 2, 1)
+            LDSP(4, 0)
+            LDSP(4, 1)
+            LDSP(4, 2)
+            LDSP(4, 3)
+            LDSP(4, 4)
+            LDSP(4, 5)
         }
         printf("BEST %s %.1f us %.1f GB/s\n", best, best_us, B3 / (best_us * 1e-6) / 1e9);
         return 0;
