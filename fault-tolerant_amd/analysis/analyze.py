@@ -226,6 +226,52 @@ def plot_sweep(t: pd.DataFrame, path: str) -> None:
     plt.close(fig)
 
 
+def _last_line(path: str) -> dict:
+    with open(path) as f:
+        return json.loads([l for l in f.read().splitlines() if l.startswith("{")][-1])
+
+
+def decisions(line: dict) -> dict:
+    """What one N > 1 bench line (the driver's node run) decides for the next build
+    (DESIGN.md 9.1): the mesh form its transport selection picked, whether the mid-size
+    gates pay (the largest size up to which every gated column beats its ungated twin:
+    FTAR_OPT_GATE_MAX), whether configs[4]'s elided step-0 copy recovered across GPUs
+    (deviation 6), which small-call setting was exact, and the north-star fractions."""
+    sel = line.get("transport_selection") or {}
+    sweep = {int(k): v for k, v in (line.get("size_sweep_us") or {}).items() if isinstance(v, dict)}
+    gate_max = 1 << 20  # the library's default
+    for b in sorted(k for k in sweep if k > (1 << 20)):
+        row = sweep[b]
+        pairs = [(row.get(f"{a}_midgate_us"), row.get(f"{a}_us")) for a in ("raben", "rd")]
+        pairs = [(g, u) for g, u in pairs if g is not None and u is not None]
+        if not pairs or any(g >= u for g, u in pairs):
+            break
+        gate_max = b
+    ns = line.get("north_star") or {}
+    c5 = line.get("c5_single_kill") or {}
+    ex = line.get("exact_on_node") or {}
+    times = {k[:-3]: v for k, v in sel.items() if k.endswith("_ms")}
+    return {
+        "n_gpus": line.get("n_gpus"),
+        "rehearsal": bool(ns.get("rehearsal")),
+        "value_GBps": line.get("value"),
+        "transport_chosen": sel.get("chosen", line.get("transport")),
+        "transport_ms": times,
+        "transport_inexact_or_failed": sorted(set(sel.get("inexact") or []) | set(sel.get("failed") or {})),
+        "never_fastest": sorted(k for k in times if k != sel.get("chosen")),
+        "gate_max_bytes": gate_max,
+        "gate_max_changes": gate_max != (1 << 20),
+        "all_exact": ex.get("all_exact"),
+        "small_call_setting": (line.get("size_sweep_us") or {}).get("small_call_setting"),
+        "dead_input_cross_device": c5.get("dead_input_cross_device"),
+        "elide_step0_copy_across_gpus": c5.get("dead_input_cross_device") == "recovered",
+        "north_star_frac": ns.get("frac"),
+        "north_star_met": ns.get("met"),
+        "reference_schedule_frac": ns.get("reference_schedule_frac"),
+        "link_GBps": (line.get("link_calibration") or {}).get("single_link_GBps"),
+    }
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -245,6 +291,8 @@ def main(argv=None) -> int:
     s = sub.add_parser("sweep")
     s.add_argument("bench_json")
     s.add_argument("--plot", default=None)
+    d = sub.add_parser("decisions", help="what the node's N > 1 bench lines decide (DESIGN.md 9.1)")
+    d.add_argument("bench_json", nargs="+")
     k = sub.add_parser("clean")
     k.add_argument("in_csv")
     k.add_argument("out_csv")
@@ -269,6 +317,9 @@ def main(argv=None) -> int:
         print(t.to_string(index=False))
         if a.plot:
             plot_sweep(t, a.plot)
+    elif a.cmd == "decisions":
+        for path in a.bench_json:
+            print(json.dumps(decisions(_last_line(path))))
     else:
         print(f"kept {clean(a.in_csv, a.out_csv, a.ns)} rows -> {a.out_csv}")
     return 0

@@ -163,3 +163,37 @@ def test_analyze_figures(tmp_path):
     a.plot_sweep(a.sweep_table(str(bj)), str(tmp_path / "sweep.png"))
     for f in ("cmp.png", "fault.png", "pie.png", "sweep.png"):
         assert (tmp_path / f).stat().st_size > 5000, f
+
+
+def test_analyze_decisions_from_a_node_line(tmp_path):
+    """`analyze.py decisions`: what a node's N > 1 line decides -- the mesh
+    form picked, the mid-size gate limit (the largest size up to which every gated column
+    beats its ungated twin), the cross-GPU elided-copy verdict, the north-star fractions."""
+    a = _analyze()
+    mb = 1 << 20
+    line = {"n_gpus": 8, "value": 2100.0, "transport": "mesh-u4",
+            "transport_selection": {"mesh_ms": 1.02, "mesh_u4_ms": 0.98, "mesh_push_ms": 1.2, "chosen": "mesh_u4",
+                                    "inexact": ["mesh_push2"], "failed": {"direct": "boom"}},
+            "size_sweep_us": {"small_call_setting": "default (gates, flag-signalled drains)", "gate": 1.0,
+                              str(mb): {"bytes": mb, "raben_us": 40, "rd_us": 60},
+                              str(2 * mb): {"bytes": 2 * mb, "raben_us": 50, "raben_midgate_us": 45, "rd_us": 70,
+                                            "rd_midgate_us": 66},
+                              str(8 * mb): {"bytes": 8 * mb, "raben_us": 80, "raben_midgate_us": 70, "rd_us": 120,
+                                            "rd_midgate_us": 110},
+                              str(16 * mb): {"bytes": 16 * mb, "raben_us": 120, "raben_midgate_us": 125, "rd_us": 200,
+                                             "rd_midgate_us": 190}},
+            "north_star": {"frac": 0.81, "met": True, "reference_schedule_frac": 0.74, "rehearsal": False},
+            "c5_single_kill": {"dead_input_cross_device": "recovered"},
+            "exact_on_node": {"all_exact": True},
+            "link_calibration": {"single_link_GBps": 64.0}}
+    p = tmp_path / "scale8.json"
+    p.write_text(json.dumps(dict(line, line="headline")) + "\n" + json.dumps(dict(line, line="final")) + "\n")
+    d = a.decisions(a._last_line(str(p)))
+    assert d["transport_chosen"] == "mesh_u4" and d["never_fastest"] == ["mesh", "mesh_push"]
+    assert d["transport_inexact_or_failed"] == ["direct", "mesh_push2"]
+    assert d["gate_max_bytes"] == 8 * mb and d["gate_max_changes"]
+    assert d["elide_step0_copy_across_gpus"] and d["north_star_met"] and d["north_star_frac"] == 0.81
+    assert d["small_call_setting"].startswith("default") and d["link_GBps"] == 64.0
+    # a gated column that loses at the first mid size keeps the library's 1 MiB
+    line["size_sweep_us"][str(2 * mb)]["rd_midgate_us"] = 71
+    assert a.decisions(line)["gate_max_bytes"] == mb
