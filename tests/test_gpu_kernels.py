@@ -290,17 +290,32 @@ def test_short_pinned_buffers_refused(ftar):
 
 @pytest.mark.timeout(300)
 def test_tree_kernels_against_oracle():
-    """The mesh's tree kernels on their own (tests/kernel_tree/tree_check.hip, built by
+    """The mesh's tree kernels on their own (tests/kernel_gpu/tree_check.hip, built by
     __graft_entry__.build()): tree_kernel at p = 2, 4, 8 AND 16 (the schedules reach p = 16
     only with 16 ranks), unroll 1 / 2 / 4, extra destinations (push2), co-aligned and
     mutually misaligned pointers, ragged lengths up to 2^20 + 7, and tree_batch_kernel (the
     one-shot form, 1 / 3 / 8 trees), float32 / float64 / int32 / int64 with SUM, PROD, MAX,
     MIN and MPI's logical / bitwise ops -- bit-exact against the balanced tree computed by
     the oracle's reduce_local, MAX / MIN over NaN, signed zeros and infinities."""
+    _run_checker("tree_check")
+
+
+def _run_checker(name, *args):
     import subprocess
-    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "kernel_tree", "_build",
-                       "tree_check")
-    assert os.path.exists(exe), "tests/kernel_tree not built: run __graft_entry__.build()"
-    cp = subprocess.run([exe], capture_output=True, text=True, timeout=280)
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "kernel_gpu", "_build",
+                       name)
+    assert os.path.exists(exe), "tests/kernel_gpu not built: run __graft_entry__.build()"
+    cp = subprocess.run([exe, *args], capture_output=True, text=True, timeout=280)
     assert cp.returncode == 0, (cp.stdout[-3000:], cp.stderr[-2000:])
-    assert "0 failed" in cp.stdout, cp.stdout[-3000:]
+    assert " 0 failed" in cp.stdout, cp.stdout[-3000:]
+
+
+@pytest.mark.timeout(300)
+def test_segment_kernel_against_oracle():
+    """The segment kernel on its own (tests/kernel_gpu/seg_check.hip): 400 random lists of
+    up to 16 copy / reduce pieces as the schedules build them -- ragged lengths up to 2^20,
+    co-aligned and misaligned pointers, a second destination holding the result or (the
+    mid-exchange guard) the local operand's pre-image, grids capped at 2^20 / 1024 / 128 / 7
+    workgroups -- bit-exact against the oracle, nothing written outside a destination,
+    sources untouched; MAX / MIN over NaN, signed zeros and infinities."""
+    _run_checker("seg_check")
