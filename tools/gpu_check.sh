@@ -74,7 +74,7 @@ fi
 if has rehearse || has rehearse8; then
   ns="2 4"; has rehearse8 && ns="8"
   for n in $ns; do
-    FTAR_DEVICE=0 FTAR_C5_RANKS=5 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+    FTAR_DEVICE=0 FTAR_C5_RANKS=${C5_RANKS:-5} timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
         --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps ${REH_STEPS:-5} \
         --warmup 1 --dist-backend gloo > "$OUT/rehearse_$n.json" 2> "$OUT/rehearse_$n.err" &
     pid=$!
