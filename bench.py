@@ -113,6 +113,14 @@ def load_package():
     return mod
 
 
+def load_analysis():
+    spec = importlib.util.spec_from_file_location(
+        "ftar_analyze", os.path.join(ROOT, "fault-tolerant_amd", "analysis", "analyze.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
 def load_tool(name):
     spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "tools", name + ".py"))
     mod = importlib.util.module_from_spec(spec)
@@ -1460,6 +1468,10 @@ def multi(args):
     line["c5_single_kill"] = c5
     line["legs"] = legs
     line["job_s"] = round(time.monotonic() - T_START, 1)
+    try:  # what this run decides for the next build (analysis/analyze.py decisions)
+        line["node_decisions"] = load_analysis().decisions(line)
+    except Exception as e:  # a summary, never the line's fate
+        line["node_decisions"] = {"error": str(e)[-200:]}
     dog.line = line
     if rank == 0:
         print(json.dumps(dict(line, line="final")), flush=True)

@@ -319,6 +319,10 @@ def test_bench_multi_headline_survives_hung_and_failing_legs(hostsim, tmp_path):
     assert fin["exact_on_node"]["all_exact"], fin["exact_on_node"]
     assert fin["int32_rank_checksum_ok"] == {"raben": True, "rd": True}
     assert fin["cpu_baseline"]["value"] and fin["cpu_baseline"]["cores"] == 2
+    # what the run decides (analysis/analyze.py decisions), in the line itself
+    nd = fin["node_decisions"]
+    assert "error" not in nd, nd
+    assert nd["n_gpus"] == 2 and nd["all_exact"] and nd["gate_max_bytes"] >= 1 << 20, nd
     # the sweep ends one point past the job's vector, as the reference's campaign (2^27 ints)
     sweep = fin["size_sweep_us"]
     assert sweep[str(8 * 65536)]["raben_us"] > 0 and sweep[str(8 * 65536)]["rd_us"] > 0, sweep
