@@ -104,3 +104,5 @@ def test_bench_two_rank_scale_path():
             rk["results_consistent"], rk
     xg = d["xgmi_probe"]  # one GPU: the probe's kernels in loopback, destinations checked
     assert xg and xg["ok"] and "loopback_copy" in xg["patterns"], xg
+    nd = d["node_decisions"]  # what the run decides, summarized in the line (analysis/analyze.py)
+    assert "error" not in nd and nd["n_gpus"] == 2 and nd["rehearsal"] and nd["all_exact"], nd
