@@ -120,3 +120,37 @@ def test_op_type_check_before_any_device_call(built):
             assert L.ftar_reduce_local(None, None, 0, dt, op, None) == 9, (dt, op)
     assert L.ftar_reduce_local(None, None, 0, 0, 10, None) == 13
     assert L.ftar_reduce_local(None, None, 0, 4, 0, None) == 13
+
+
+def test_python_structs_mirror_the_header(tmp_path):
+    """The ctypes mirrors of the header's structs (fault-tolerant_amd/__init__.py: Stats, Kill)
+    have the C layout field for field -- a field added on one side only would shift every
+    later one silently.  Offsets and sizes from a C program compiled against include/ftar.h."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ftar_abi_mirror", os.path.join(ROOT, "fault-tolerant_amd",
+                                                                                 "__init__.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    src = open(HEADER).read()
+    checks = []
+    for cls, cname in ((m.Stats, "ftar_stats"), (m.Kill, "ftar_kill")):
+        body = re.search(r"typedef struct\s*\{([^{}]*)\}\s*" + cname + r"\s*;", re.sub(r"/\*.*?\*/", "", src, flags=re.S))
+        assert body, cname
+        cfields = re.findall(r"(\w+)\s*;", body.group(1))
+        assert [f for f, _ in cls._fields_] == cfields, (cname, cfields)
+        checks.append((cls, cname, cfields))
+    prog = tmp_path / "layout.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ftar.h"', "int main(void) {"]
+    for _, cname, cfields in checks:
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        lines += [f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));' for f in cfields]
+    lines.append("return 0; }")
+    prog.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                       check=True).stdout.splitlines())
+    for cls, cname, cfields in checks:
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f in cfields:
+            assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
