@@ -506,3 +506,29 @@ def test_host_entry_pinned_zero_copy(oracle, algo, p, kills, env):
     ins = oracle.random_inputs(p, 65536 + 9, seed=p * 13 + len(kills))
     _check(oracle.recursive_doubling if algo == "rd" else oracle.rabenseifner, algo, ins, kills,
            env=dict(env, FTAR_PROBE_PINNED="1"))
+
+
+# The stated float tolerance (north_star "within a stated tolerance for float
+# SUM"): bit-exact against the oracle's tree (the tests above), and against the exact sum
+# |err_i| <= gamma(depth) * sum_r |x_r[i]| per element, gamma(d) = d u / (1 - d u), u = 2^-24
+# (the standard bound of a summation tree of height d in round-to-nearest), depth = the
+# reduction tree's height (ceil(log2 p): the pre-step of a non-power-of-two p adds one level).
+FLOAT_TOL_UNIT = 2.0 ** -24
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [2, 5, 8])
+def test_float_sum_within_stated_tolerance(oracle, algo, p):
+    """float32 SUM of uniform [-1, 1) vectors (1 Mi + 3 elements per rank) against the exact
+    sum in float64: every element within gamma(depth) x sum |x|, on every rank."""
+    ins = oracle.random_inputs(p, (1 << 20) + 3, seed=300 + p)
+    r = H.run_probe(algo, ins, backend="gpu", devmap=ALL_ON_GPU0, timeout=240)
+    assert r.returncode == 0 and not r.aborted, r.stderr[-2000:]
+    exact = np.sum([x.astype(np.float64) for x in ins], axis=0)
+    mag = np.sum([np.abs(x.astype(np.float64)) for x in ins], axis=0)
+    depth = int(np.ceil(np.log2(p)))
+    bound = depth * FLOAT_TOL_UNIT / (1 - depth * FLOAT_TOL_UNIT) * mag
+    for w in range(p):
+        err = np.abs(r.outputs[w][0].astype(np.float64) - exact)
+        assert (err <= bound).all(), (w, float((err / np.maximum(bound, 1e-300)).max()))
