@@ -160,6 +160,8 @@ struct ftar_dev {
     unsigned *gate_dw;
     unsigned big_blocks;
     int big_pending;               // the pending gated launch is a relayed (mid-size) one
+    unsigned relay_min;            // FTAR_GATE_RELAY_MIN: short gated launches of this many workgroups or
+                                   // more relay their gate too (one PCIe poller instead of one per workgroup)
 };
 
 extern "C" {
@@ -254,6 +256,9 @@ int fdev_open(int device, ftar_dev **out)
             const char *bb = getenv("FTAR_GATE_BIG_BLOCKS");
             long v = bb ? atol(bb) : (long)prop.multiProcessorCount / 2;
             d->big_blocks = (unsigned)(v < 1 ? 1 : v);
+            const char *rm = getenv("FTAR_GATE_RELAY_MIN");
+            long r = rm ? atol(rm) : 2;
+            d->relay_min = (unsigned)(r < 1 ? 1 : r);
         }
         if (d->flag_sync) {
             HIPCHK(hipEventCreateWithFlags(&d->fence_pre, hipEventDisableTiming)); // fenced, see sync_stream
@@ -650,6 +655,17 @@ static ftar::KSignal arm_gate(ftar_dev *d, double link, double hbm)
                          gate_err(d, d->gate_seq), d->gate_ticks};
 }
 
+// A short gated launch of several workgroups waits with ONE of them polling the host word
+// over PCIe, the others polling the device word it relays the verdict through (the relayed
+// form of the mid-size launches, signal_gate): up to 64 uncached PCIe pollers per launch
+// slowed the peers sharing a GPU 2x at 1 MiB (RD, 4 ranks: 194 vs 93 us ungated).
+static void relay_gate(ftar_dev *d, ftar::KSignal &sig, unsigned grid)
+{
+    if (!d->gate_dw || grid < d->relay_min) return;
+    sig.gate_poll = d->gate_dw + d->gate_seq % ftar::kGateSlots;
+    sig.gate_dev = d->gate_dw + 32 + d->gate_seq % ftar::kGateSlots;
+}
+
 // Keep the plan of the gate just armed (d->gate_seq) for a relaunch: the same launch with
 // no signal, gate or staging phase.
 static void keep_plan(ftar_dev *d, int batch, int dtype, int op, int nsrc, unsigned grid, const ftar::KSegList *L,
@@ -727,6 +743,7 @@ int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *con
         d->ctr.hbm_bytes += 2.0 * (double)stage_n * (double)es;
     }
     B.sig = arm_gate(d, link, hbm);
+    relay_gate(d, B.sig, grid);
     keep_plan(d, 1, dtype, op, nsrc, grid, nullptr, &B);
     if (stage_tag) {
         B.sig.stage_src = stage_src;
@@ -904,6 +921,7 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
         d->ctr.hbm_bytes += 2.0 * (double)stage_n * (double)es;
     }
     L.sig = arm_gate(d, link, hbm);
+    relay_gate(d, L.sig, grid);
     keep_plan(d, 0, dtype, op, 0, grid, &L, nullptr);
     if (stage_tag) {
         L.sig.stage_src = stage_src;
