@@ -42,11 +42,11 @@ struct KSignal {
     unsigned gate_val;
     unsigned *err;        // pinned host word of this gate's slot: set to gate_val on a gate timeout
     unsigned long long gate_ticks;
-    // Relayed gate (a mid-size launch of many workgroups, queued behind a fenced marker
-    // instead of signalling): only the first workgroup to start -- elected by an atomic max
-    // of gate_val into *gate_poll -- polls the host word; it relays the verdict through the
-    // device word *gate_dev, which the other workgroups poll.  nullptr = every workgroup
-    // polls the host word itself (the short launches).
+    // Relayed gate (every gated launch of FTAR_GATE_RELAY_MIN = 2 workgroups or more: the short
+    // signalling ones and the mid-size ones queued behind a fenced marker): only the first
+    // workgroup to start -- elected by an atomic max of gate_val into *gate_poll -- polls the
+    // host word over PCIe; it relays the verdict through the device word *gate_dev, which the
+    // other workgroups poll.  nullptr = the workgroup polls the host word itself.
     unsigned *gate_poll;
     unsigned *gate_dev;
     // Optional staging phase BEFORE the gate (a gated launch that also stages this rank's
