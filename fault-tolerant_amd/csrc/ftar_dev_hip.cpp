@@ -729,7 +729,14 @@ int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *con
     unsigned grid = 0;
     double link, hbm;
     int rc = build_batch(d, dtype, op, src, nsrc, remote_mask, out, n, ntree, tag, &B, &grid, &link, &hbm);
-    if (rc || !can_gate(d, grid)) return rc;
+    if (rc) return rc;
+    // a one-shot of up to 4x the signal limit's workgroups still waits at its gate: its vector
+    // workgroups take several chunks each (cap_tree_batch; the same tree per element)
+    if (grid > d->flag_max && grid <= 4 * d->flag_max) {
+        const unsigned g = ftar::cap_tree_batch(&B, d->flag_max);
+        if (g) grid = g;
+    }
+    if (!can_gate(d, grid)) return 0;
     // only a launch that never writes what it reads is gated: a gate the device gave up on
     // is relaunched whole, and some workgroups may have run already
     const size_t es = esize_of(dtype);

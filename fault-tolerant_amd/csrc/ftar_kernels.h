@@ -162,6 +162,9 @@ struct TreeBatch {
     KSignal sig; // optional completion signal
 };
 unsigned plan_tree_batch(TreeBatch *B, int p, size_t esize, unsigned max_blocks);
+// shrinks a planned batch to at most max_total workgroups by giving each vector workgroup
+// several chunks (its scalar workgroups stay); the new grid, or 0 if it cannot fit
+unsigned cap_tree_batch(TreeBatch *B, unsigned max_total);
 hipError_t launch_tree_batch(int dtype, int op, int p, const TreeBatch &B, unsigned grid, hipStream_t s);
 
 unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_blocks, KSegList *L);

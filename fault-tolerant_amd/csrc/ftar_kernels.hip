@@ -387,24 +387,28 @@ template <typename T, int OP, int P, int U>
 __device__ __forceinline__ void tree_body(const TreeArgs &A, unsigned b, unsigned nblocks)
 {
     if (b < A.nvb) {
-        const size_t i0 = (size_t)b * kBlock * U + threadIdx.x;
-        if (i0 + (size_t)(U - 1) * kBlock < A.nv) {
-            uint4 v[U][P];
+        // chunk b, then b + nvb, ... (once, unless the planner capped the vector workgroups:
+        // cap_tree_batch, a gated one-shot launch that must stay within the signal limit)
+        for (size_t c = b; c * kBlock * U < A.nv; c += A.nvb) {
+            const size_t i0 = c * kBlock * U + threadIdx.x;
+            if (i0 + (size_t)(U - 1) * kBlock < A.nv) {
+                uint4 v[U][P];
 #pragma unroll
-            for (int u = 0; u < U; u++)
+                for (int u = 0; u < U; u++)
 #pragma unroll
-                for (int j = 0; j < P; j++)
-                    v[u][j] = ldnt((const uint4 *)((const T *)A.src[j] + A.head) + i0 + (size_t)u * kBlock);
+                    for (int j = 0; j < P; j++)
+                        v[u][j] = ldnt((const uint4 *)((const T *)A.src[j] + A.head) + i0 + (size_t)u * kBlock);
 #pragma unroll
-            for (int u = 0; u < U; u++) tree_store<T, OP, P>(A, i0 + (size_t)u * kBlock, v[u]);
-        } else {
-            for (int u = 0; u < U; u++) {
-                const size_t i = i0 + (size_t)u * kBlock;
-                if (i >= A.nv) break;
-                uint4 v[P];
+                for (int u = 0; u < U; u++) tree_store<T, OP, P>(A, i0 + (size_t)u * kBlock, v[u]);
+            } else {
+                for (int u = 0; u < U; u++) {
+                    const size_t i = i0 + (size_t)u * kBlock;
+                    if (i >= A.nv) break;
+                    uint4 v[P];
 #pragma unroll
-                for (int j = 0; j < P; j++) v[j] = ldnt((const uint4 *)((const T *)A.src[j] + A.head) + i);
-                tree_store<T, OP, P>(A, i, v);
+                    for (int j = 0; j < P; j++) v[j] = ldnt((const uint4 *)((const T *)A.src[j] + A.head) + i);
+                    tree_store<T, OP, P>(A, i, v);
+                }
             }
         }
         return;
@@ -530,6 +534,35 @@ unsigned plan_tree_batch(TreeBatch *B, int p, size_t esize, unsigned max_blocks)
         unsigned g = plan_tree(&B->t[k], p, esize, max_blocks);
         if (g == 0) return 0;
         total += g;
+    }
+    B->first[B->nt] = total;
+    return total;
+}
+
+unsigned cap_tree_batch(TreeBatch *B, unsigned max_total)
+{
+    unsigned sb = 0, vb = 0, trees_v = 0;
+    for (int k = 0; k < B->nt; k++) {
+        vb += B->t[k].nvb;
+        sb += B->first[k + 1] - B->first[k] - B->t[k].nvb;
+        trees_v += B->t[k].nvb > 0;
+    }
+    if (vb + sb <= max_total) return vb + sb;
+    if (sb + trees_v > max_total) return 0;
+    const unsigned avail = max_total - sb;
+    unsigned nvb[kMaxBatch], total = 0;
+    for (int k = 0; k < B->nt; k++) {
+        nvb[k] = B->t[k].nvb ? (unsigned)((unsigned long long)B->t[k].nvb * avail / vb) : 0;
+        if (B->t[k].nvb && nvb[k] < 1) nvb[k] = 1;
+        total += nvb[k] + (B->first[k + 1] - B->first[k] - B->t[k].nvb);
+    }
+    if (total > max_total) return 0; // unchanged
+    total = 0;
+    for (int k = 0; k < B->nt; k++) {
+        const unsigned s = B->first[k + 1] - B->first[k] - B->t[k].nvb;
+        B->first[k] = total;
+        B->t[k].nvb = nvb[k];
+        total += nvb[k] + s;
     }
     B->first[B->nt] = total;
     return total;

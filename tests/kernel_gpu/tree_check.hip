@@ -9,7 +9,8 @@
 // oracle's reduce_local (oracle/ftar_oracle.c, OpenMPI's operand roles: inout op in), so
 // the operand order of every combination is pinned (MAX / MIN over NaN, signed zeros and
 // infinities).  Lengths ragged and co-aligned (vector body + scalar head / tail) or not
-// (scalar path), unroll 1 / 2 / 4.
+// (scalar path), unroll 1 / 2 / 4; batches also capped to 64 / 9 workgroups (cap_tree_batch:
+// each vector workgroup loops over several chunks, as a gated one-shot launch runs).
 //   tree_check [quick|swapped]   prints one line per failing case, then "tree_check: N cases, F failed";
 //   `swapped` checks against the tree with every combination's operands swapped -- the
 //   checker's own test: MAX / MIN cases must then fail
@@ -171,7 +172,7 @@ static void run_tree(const Case &c, std::mt19937_64 &g)
 }
 
 // the one-shot form: ntree trees of p sources each in one launch (tree k owns its workgroups)
-static void run_batch(const Case &c, int ntree, std::mt19937_64 &g)
+static void run_batch(const Case &c, int ntree, std::mt19937_64 &g, unsigned cap = 0)
 {
     const size_t es = esize(c.dt);
     ftar::TreeBatch B;
@@ -200,7 +201,11 @@ static void run_batch(const Case &c, int ntree, std::mt19937_64 &g)
         B.t[k].unroll = 1;
         bufs.push_back(o);
     }
-    const unsigned grid = ftar::plan_tree_batch(&B, c.p, es, 1u << 20);
+    unsigned grid = ftar::plan_tree_batch(&B, c.p, es, 1u << 20);
+    if (grid && cap && grid > cap) { // the gated one-shot's capped grid: vector workgroups loop
+        const unsigned gc = ftar::cap_tree_batch(&B, cap);
+        if (gc) grid = gc;
+    }
     if (grid == 0) {
         printf("FAIL plan_tree_batch refused p %d n %zu\n", c.p, c.n);
         g_fail++;
@@ -246,7 +251,8 @@ int main(int argc, char **argv)
         for (int p : {2, 4, 8})
             for (size_t n : {(size_t)5, (size_t)4099, (size_t)(1u << 16) + 3})
                 for (int nt : {1, 3, 8})
-                    run_batch(Case{o[0], o[1], p, 1, n, 0, 0}, nt, g);
+                    for (unsigned cap : {0u, 64u, 9u})
+                        run_batch(Case{o[0], o[1], p, 1, n, 0, 0}, nt, g, cap);
     printf("tree_check: %d cases, %d failed\n", g_cases, g_fail);
     return g_fail ? 1 : 0;
 }
