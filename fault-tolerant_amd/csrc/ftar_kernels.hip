@@ -156,10 +156,30 @@ __device__ __forceinline__ void stage_copy(const KSignal &G)
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < G.stage_n; i += stride) d[i] = s[i];
 }
 
+// 16-byte vectors when both ends are 16-byte aligned (the workspace and a hipMalloc'd input
+// are), the elements past the last whole vector one by one
+__device__ __forceinline__ bool stage_copy_vec(const KSignal &G)
+{
+    if ((((uintptr_t)G.stage_src | (uintptr_t)G.stage_dst) & 15) != 0) return false;
+    const size_t nv = G.stage_n * G.stage_es / 16;
+    const uint4 *s = (const uint4 *)G.stage_src;
+    uint4 *d = (uint4 *)G.stage_dst;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) d[i] = s[i];
+    const size_t done = nv * 16 / G.stage_es; // elements copied as vectors
+    if (blockIdx.x == 0)
+        for (size_t i = done + threadIdx.x; i < G.stage_n; i += blockDim.x) {
+            if (G.stage_es == 8) ((unsigned long long *)G.stage_dst)[i] = ((const unsigned long long *)G.stage_src)[i];
+            else ((unsigned *)G.stage_dst)[i] = ((const unsigned *)G.stage_src)[i];
+        }
+    return true;
+}
+
 __device__ __forceinline__ void signal_stage(const KSignal &G)
 {
     if (!G.stage_dst) return;
-    if (G.stage_es == 8) stage_copy<unsigned long long>(G);
+    if (stage_copy_vec(G)) {
+    } else if (G.stage_es == 8) stage_copy<unsigned long long>(G);
     else stage_copy<unsigned>(G);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
