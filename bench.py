@@ -719,7 +719,8 @@ def _fraction(bound_s, t_s):
     return {"frac": round(r, 4), "met": r >= NORTH_STAR_FRAC}
 
 
-def north_star_block(world, S, t_head, transport, link_gbps, links, head_bytes_per_link, t_ref=None, rehearsal=False):
+def north_star_block(world, S, t_head, transport, link_gbps, links, head_bytes_per_link, t_ref=None, rehearsal=False,
+                     breakdown=None):
     """BASELINE.json north_star / SURVEY.md 8d: >= 70 % of the xGMI-bound roofline for the
     device-resident Rabenseifner Allreduce of 256 MiB float32 at 8 GPUs.
 
@@ -733,7 +734,12 @@ def north_star_block(world, S, t_head, transport, link_gbps, links, head_bytes_p
         2.25 S at p = 8 -- SURVEY.md 8d's roofline) timed in the same job, against that bound;
       * `speedup_vs_survey_roofline`: SURVEY's FT roofline time over the headline time -- how
         much faster the schedule that ran is than the reference's schedule could ever be on
-        one link per step.  A speed-up, never a fraction: it exceeds 1 by design."""
+        one link per step.  A speed-up, never a fraction: it exceeds 1 by design;
+      * `non_kernel_ms` (from `breakdown`, the profiled pass of the headline): the call's time
+        outside its kernels -- host drains, agree + barrier rounds, launch latency -- beside
+        `kernels_ms`, and `frac_kernels_only`: the schedule's bound over the kernels' time, the
+        fraction the call would reach with no time outside kernels (at
+        the 70 % target, 1.25 ms per call, every 0.1 ms outside kernels costs ~6 points)."""
     L = world.bit_length() - 1
     ft_bytes = (2.5 - 2.0 ** (1 - L)) * S
     priced = {}
@@ -775,6 +781,76 @@ def north_star_block(world, S, t_head, transport, link_gbps, links, head_bytes_p
         out["reference_shape_ms"] = round(t_ref * 1e3, 4)
         out["reference_schedule_frac"] = b["reference_schedule"]["frac"]
         out["reference_schedule_met"] = b["reference_schedule"]["met"]
+    if breakdown and breakdown.get("call_ms") is not None and breakdown.get("kernels_ms") is not None:
+        call_ms, kern_ms = breakdown["call_ms"], breakdown["kernels_ms"]
+        nk = max(0.0, call_ms - kern_ms)
+        out["call_ms_profiled"] = call_ms
+        out["kernels_ms"] = kern_ms
+        out["non_kernel_ms"] = round(nk, 4)
+        out["non_kernel_share"] = round(nk / call_ms, 4) if call_ms > 0 else None
+        out["non_kernel_parts_ms"] = {"agree_barrier_wait": breakdown.get("agree_barrier_wait_ms"),
+                                      "stream_drain_wait": breakdown.get("stream_drain_wait_ms")}
+        t_sched = head_bytes_per_link / ((link_gbps or SURVEY_LINK_GBS) * 1e9)
+        kf = _fraction(t_sched, kern_ms * 1e-3) if kern_ms > 0 and not rehearsal else {"frac": None}
+        out["frac_kernels_only"] = kf["frac"]
+    return out
+
+
+def rd_roofline_block(world, S, t_rd, transport, link_gbps, t_direct=None, rehearsal=False, breakdown=None):
+    """configs[2]: fault-tolerant recursive doubling, S bytes per rank, against link rooflines.
+
+    The reference moves one whole buffer per step over ONE partner link (MPI_Sendrecv of the
+    full vector, /root/reference/src/rd/recursive_doubling.c:21-37): L = log2(p') steps, plus
+    the pre-step (reduce_pow2, rd/util.c:3-34: an extra rank sends its vector) and the fan-out
+    to the extra ranks (recursive_doubling.c:78-89) when p is not a power of two -- so
+    (L + 2 [rem > 0]) S per rank and direction, one link at a time.  That is also the build's
+    `direct` transport.  The 2-hop relay stripes each step over r - 1 links (r = p' receivers)
+    and moves 2 S / r over each (two phases), so its bound is (2 L / r) S per link (+ the
+    direct pre / post steps).  Every fraction is a bound over the time of the schedule it
+    bounds (`_fraction`: never above 1); `reference_schedule_frac` prices the reference's
+    movement against the direct transport's own time (the same data movement, timed in the
+    same job by the RD transport selection)."""
+    L = world.bit_length() - 1
+    r = 1 << L
+    rem = world - r
+    ref_bytes = (L + (2 if rem else 0)) * float(S)
+    if transport == "relay2hop":
+        per_link = L * 2.0 / r * S + (2 if rem else 0) * float(S)
+        links = r - 1
+    else:
+        per_link, links = ref_bytes, 1
+    priced = {}
+    for tag, b in (("calibrated", link_gbps), ("nominal_76.8_assumed", XGMI_LINK_GBS),
+                   ("survey_153.6_assumed", SURVEY_LINK_GBS)):
+        if not b:
+            continue
+        t_sched = per_link / (b * 1e9)
+        t_refb = ref_bytes / (b * 1e9)
+        row = {"link_GBps": round(b, 2), "schedule_t_roof_ms": round(t_sched * 1e3, 4),
+               "schedule": {"frac": None, "met": None} if rehearsal else _fraction(t_sched, t_rd),
+               "reference_t_roof_ms": round(t_refb * 1e3, 4),
+               "speedup_vs_reference_roofline": None if rehearsal else round(t_refb / t_rd, 4)}
+        if t_direct:
+            row["reference_schedule"] = {"frac": None, "met": None} if rehearsal else _fraction(t_refb, t_direct)
+        priced[tag] = row
+    basis = "calibrated" if "calibrated" in priced else "survey_153.6_assumed"
+    b = priced[basis]
+    out = {"config": "configs[2]: FT recursive doubling, float32 SUM, one rank per GPU",
+           "transport": transport, "schedule_bytes_per_link": per_link, "links": links,
+           "reference_bytes_per_rank": ref_bytes,
+           "reference_definition": f"(L + 2 [p not a power of two]) S = {ref_bytes:.0f} B per rank and direction, "
+                                   "one partner link per step (rd/recursive_doubling.c:21-37)",
+           "basis": basis, "frac": b["schedule"]["frac"], "ms_per_step": round(t_rd * 1e3, 4),
+           "speedup_vs_reference_roofline": b["speedup_vs_reference_roofline"], "priced": priced,
+           "rehearsal": rehearsal}
+    if "bound_violated" in b["schedule"]:
+        out["bound_violated"] = b["schedule"]["bound_violated"]
+    if t_direct:
+        out["direct_ms"] = round(t_direct * 1e3, 4)
+        out["reference_schedule_frac"] = b["reference_schedule"]["frac"]
+    if breakdown and breakdown.get("call_ms") is not None and breakdown.get("kernels_ms") is not None:
+        out["non_kernel_ms"] = round(max(0.0, breakdown["call_ms"] - breakdown["kernels_ms"]), 4)
+        out["kernels_ms"] = breakdown["kernels_ms"]
     return out
 
 
@@ -843,7 +919,7 @@ def multi(args):
         dist.barrier()
         sync()
         t0 = time.perf_counter()
-        step0 = kern = syncw = drain = 0.0
+        step0 = kern = syncw = drain = gl = gh = 0.0
         for _ in range(steps):
             fn()
             st = comm.last_stats()
@@ -851,15 +927,21 @@ def multi(args):
             kern += st.kernel_ms
             syncw += st.sync_wait_s
             drain += st.drain_s
+            gl += st.gated_launches - st.gated_skips
+            gh += st.gate_holds
         sync()
         t1 = time.perf_counter()
         dist.barrier()
-        t, k, kall, sw, dr = max_over_ranks([t1 - t0, step0, kern, syncw, drain])
+        t, k, kall, sw, dr, gl, gh = max_over_ranks([t1 - t0, step0, kern, syncw, drain, gl, gh])
         timed.link_bytes = comm.last_stats().step0_link_bytes
         # where a call's time goes (max over ranks of each part, per call)
         timed.breakdown = {"call_ms": round(t / steps * 1e3, 4), "kernels_ms": round(kall / steps, 4),
                            "dominant_kernel_ms": round(k / steps, 4), "agree_barrier_wait_ms": round(sw / steps * 1e3, 4),
-                           "stream_drain_wait_ms": round(dr / steps * 1e3, 4)}
+                           "stream_drain_wait_ms": round(dr / steps * 1e3, 4),
+                           # gated launches that ran, and those given up at a barrier that waited
+                           # past FTAR_GATE_HOLD_US (max over ranks, all timed calls): a gated row
+                           # mostly given up measures the hold, not the gate
+                           "gated_launches": int(gl), "gate_holds": int(gh)}
         return t / steps, k / steps
 
     def timed_split(fn):
@@ -1085,7 +1167,8 @@ def multi(args):
             # the headline call of the profiled pass split into device time (all kernels /
             # the dominant one) and the host's waits (agree + barrier rounds, stream drains)
             "call_breakdown": breakdown,
-            "north_star": north_star_block(world, S, t_rb, transport, b_link, links, per_link, t_ref, rehearsal),
+            "north_star": north_star_block(world, S, t_rb, transport, b_link, links, per_link, t_ref, rehearsal,
+                                           breakdown),
             "schedule_link_roofline": {"schedule_bytes_per_rank": sched_bytes, "bytes_per_link": per_link,
                                        "links_per_step": links,
                                        "link_GBps": b_price,
@@ -1285,6 +1368,7 @@ def multi(args):
             set_opts([chosen_opts[o] for o in opts])
 
     rd_selection = None
+    rd_raw = {}
 
     def rd_leg():
         # recursive doubling has no mesh form (it can recover at any p): relay or direct
@@ -1300,10 +1384,14 @@ def multi(args):
                 rd_selection = {"relay2hop_ms": round(t_r * 1e3, 4), "direct_ms": round(t_d * 1e3, 4),
                                 "chosen": "relay2hop" if t_r <= t_d else "direct"}
             t_rd, k_rd = timed_split(rd)
+            rd_raw.update(t=t_rd, breakdown=timed_split.breakdown,
+                          transport="relay2hop" if comm.last_stats().relayed_steps > 0 else "direct",
+                          t_direct=t_d if rd_selection else (t_rd if world == 2 else None))
         finally:
             comm.set_option(ftar.OPT_RELAY, relay_for_raben)
         return {"ms_per_step": round(t_rd * 1e3, 4), "algbw_GBps": round(S / t_rd / 1e9, 2),
                 "value": round(world * S / t_rd / 1e9, 2), "step0_kernel_ms": round(k_rd, 4),
+                "transport": rd_raw["transport"], "call_breakdown": timed_split.breakdown,
                 "transport_selection": rd_selection}
 
     def rccl_leg():
@@ -1398,7 +1486,10 @@ def multi(args):
                             row[name + "_split_us"] = {
                                 "drain": round(timed.breakdown["stream_drain_wait_ms"] * 1e3, 2),
                                 "agree_barrier": round(timed.breakdown["agree_barrier_wait_ms"] * 1e3, 2),
-                                "gated_launches": comm.last_stats().gated_launches}
+                                "gated_launches": timed.breakdown["gated_launches"],
+                                "gate_holds": timed.breakdown["gate_holds"]}
+                        if name.endswith("_midgate") or timed.breakdown["gate_holds"]:
+                            row[name + "_gate_holds"] = timed.breakdown["gate_holds"]
                     finally:
                         comm.set_option(ftar.OPT_ONESHOT_MAX, oneshot_max)
                         comm.set_option(ftar.OPT_GATE_MAX, gate_max0)
@@ -1464,6 +1555,12 @@ def multi(args):
     # calls that found the caller's stream busy and waited for it on the host
     final["user_stream_waits_max_over_ranks"] = int(max_over_ranks([float(comm.last_stats().user_stream_waits)])[0])
     line = build_line(transports, t_ref, k_ref)
+    if final.get("rd") and rd_raw.get("t"):
+        # configs[2] against its link rooflines, priced at the same link as the headline
+        cal = link_cal_from(transports)
+        final["rd"]["schedule_link_roofline"] = rd_roofline_block(
+            world, S, rd_raw["t"], rd_raw["transport"], cal["single_link_GBps"] if cal and not rehearsal else None,
+            rd_raw.get("t_direct"), rehearsal, rd_raw.get("breakdown"))
     line.update(final)
     line["c5_single_kill"] = c5
     line["legs"] = legs

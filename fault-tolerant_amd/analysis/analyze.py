@@ -251,6 +251,7 @@ def decisions(line: dict) -> dict:
     c5 = line.get("c5_single_kill") or {}
     ex = line.get("exact_on_node") or {}
     times = {k[:-3]: v for k, v in sel.items() if k.endswith("_ms")}
+    rdl = (line.get("rd") or {}).get("schedule_link_roofline") or {}
     return {
         "n_gpus": line.get("n_gpus"),
         "rehearsal": bool(ns.get("rehearsal")),
@@ -268,6 +269,11 @@ def decisions(line: dict) -> dict:
         "north_star_frac": ns.get("frac"),
         "north_star_met": ns.get("met"),
         "reference_schedule_frac": ns.get("reference_schedule_frac"),
+        "north_star_non_kernel_ms": ns.get("non_kernel_ms"),
+        "north_star_frac_kernels_only": ns.get("frac_kernels_only"),
+        "rd_transport": rdl.get("transport"),
+        "rd_frac": rdl.get("frac"),
+        "rd_reference_schedule_frac": rdl.get("reference_schedule_frac"),
         "link_GBps": (line.get("link_calibration") or {}).get("single_link_GBps"),
     }
 

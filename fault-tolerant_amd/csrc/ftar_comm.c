@@ -155,7 +155,13 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->overlap = getenv("FTAR_OVERLAP") ? atoi(getenv("FTAR_OVERLAP")) : 1;
     c->relay = getenv("FTAR_RELAY") ? atoi(getenv("FTAR_RELAY")) : 1;
     c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 2;
-    if (c->redundancy < 0 || c->redundancy > 2) c->redundancy = 2;
+    if (c->redundancy < 0 || c->redundancy > 2) {
+        /* the same values ftar_comm_set_option accepts (it refuses others with FTAR_ERR_ARG) */
+        fprintf(stderr, "ftar: rank %d: FTAR_REDUNDANCY=%s is not 0, 1 or 2: refused\n", rank,
+                getenv("FTAR_REDUNDANCY"));
+        free(c);
+        return FTAR_ERR_ARG;
+    }
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
     c->push = getenv("FTAR_PUSH") ? atoi(getenv("FTAR_PUSH")) : 0;
@@ -180,7 +186,9 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
         free(c);
         return rc;
     }
-    rc = ftar_ctrl_join(&c->job, device);
+    char phys[32];
+    if (fdev_physical_id(c->dev, phys, sizeof(phys))) phys[0] = 0;
+    rc = ftar_ctrl_join(&c->job, device, phys);
     if (rc) {
         fdev_close(c->dev);
         ftar_ctrl_detach(&c->job);
@@ -340,7 +348,7 @@ void ftar_resolve_inputs(ftar_comm *c)
             c->export_user = 0;
             me->uid = 0; /* this call's input is the staged IN from here on (ftar_dead_input) */
             if (c->in_alias) { /* stage the whole vector: what every schedule reads from IN */
-                fdev_seg s = {FDEV_COPY, 0, c->ws[WS_IN], c->in_alias, NULL, c->in_bytes / 4, NULL};
+                fdev_seg s = {FDEV_COPY, 0, c->ws[WS_IN], c->in_alias, NULL, c->in_bytes / 4, NULL, 0};
                 ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL);
                 ftar_drain(c);
             }
@@ -503,7 +511,7 @@ uint64_t ftar_step_sync(ftar_comm *c, int nsteps)
         while (now_s() - t0 < d) {
             if (c->pad_src && c->pad) {
                 size_t n = c->pad_bytes < FTAR_PAD_BYTES ? c->pad_bytes : FTAR_PAD_BYTES;
-                fdev_seg s = {FDEV_COPY, FDEV_REMOTE_X, c->pad, c->pad_src, NULL, n / 4, NULL};
+                fdev_seg s = {FDEV_COPY, FDEV_REMOTE_X, c->pad, c->pad_src, NULL, n / 4, NULL, 0};
                 const void *src = c->pad_src;
                 if (n / 4 == 0 || ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL)) break;
                 ftar_drain(c);
@@ -578,10 +586,17 @@ int64_t ftar_peer_pub(ftar_comm *c, int w)
 
 int ftar_is_dead(ftar_comm *c, int w) { return ftar_ctrl_is_dead(&c->job, w); }
 
+/* Physical identities, not HIP ordinals: under per-rank HIP_VISIBLE_DEVICES /
+ * ROCR_VISIBLE_DEVICES masks every rank may see its own GPU as device 0.  A
+ * slot without an identity falls back to the ordinal. */
 int ftar_spans_devices(const ftar_comm *c)
 {
-    for (int i = 0; i < c->size; i++)
-        if (c->job.shm->slot[c->order[i]].device != c->job.shm->slot[c->order[0]].device) return 1;
+    const ftar_slot *a = &c->job.shm->slot[c->order[0]];
+    for (int i = 1; i < c->size; i++) {
+        const ftar_slot *b = &c->job.shm->slot[c->order[i]];
+        if (a->phys[0] && b->phys[0] ? strncmp(a->phys, b->phys, sizeof(a->phys)) != 0 : a->device != b->device)
+            return 1;
+    }
     return 0;
 }
 void ftar_enter(ftar_comm *c) { ftar_ctrl_enter(&c->job); }
@@ -644,7 +659,8 @@ int ftar_prelaunch(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int ns
 static int seg_eq(const fdev_seg *a, const fdev_seg *b)
 {
     return a->kind == b->kind && a->remote == b->remote && a->out == b->out && a->x == b->x &&
-           (a->kind == FDEV_COPY || a->y == b->y) && a->n == b->n && a->out2 == b->out2;
+           (a->kind == FDEV_COPY || a->y == b->y) && a->n == b->n && a->out2 == b->out2 &&
+           (!a->out2 || a->out2_pre == b->out2_pre);
 }
 
 void ftar_run_gated_or(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
@@ -742,7 +758,7 @@ int ftar_single_rank(ftar_comm *c, const void *sbuf, void *rbuf, size_t bytes)
     ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BEFORE);
     ftar_enter(c);
     if (sbuf != rbuf) {
-        fdev_seg s = {FDEV_COPY, 0, rbuf, sbuf, NULL, bytes / 4, NULL};
+        fdev_seg s = {FDEV_COPY, 0, rbuf, sbuf, NULL, bytes / 4, NULL, 0};
         ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL);
     }
     ftar_launched(c, FTAR_PH_PRE, 0);

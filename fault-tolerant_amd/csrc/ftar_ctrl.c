@@ -126,7 +126,7 @@ int ftar_ctrl_attach(ftar_job *job, const char *name, int rank, int size, int cr
     return FTAR_SUCCESS;
 }
 
-int ftar_ctrl_join(ftar_job *job, int device)
+int ftar_ctrl_join(ftar_job *job, int device, const char *phys)
 {
     ftar_slot *s = &job->shm->slot[job->rank];
     pthread_mutexattr_t a;
@@ -137,6 +137,7 @@ int ftar_ctrl_join(ftar_job *job, int device)
     pthread_mutexattr_destroy(&a);
     if (pthread_mutex_lock(&s->alive) != 0) return FTAR_ERR_STATE;
     s->device = device;
+    snprintf(s->phys, sizeof(s->phys), "%s", phys ? phys : "");
     atomic_store(&s->pid, (int)getpid());
     atomic_store(&s->arrive, 0);
     atomic_store_explicit(&s->state, FTAR_SLOT_RUNNING, memory_order_release);

@@ -25,7 +25,7 @@
 #include "ftar_dev.h"
 
 #define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
-#define FTAR_SHM_VERSION 4
+#define FTAR_SHM_VERSION 5
 #define FTAR_NBUF 4       /* exported workspace buffers per rank (IN, W, T, R) */
 #define FTAR_DECISIONS 64 /* ring of agree decisions */
 
@@ -43,7 +43,9 @@ typedef struct {
     pthread_mutex_t alive;          /* robust + pshared, locked by the owner while alive */
     _Atomic int state;              /* FTAR_SLOT_* */
     _Atomic int pid;
-    int device;
+    int device;                     /* HIP ordinal in the rank's process (its visibility mask applies) */
+    char phys[32];                  /* physical device identity (PCI bus id): ordinals of ranks with
+                                       different HIP_VISIBLE_DEVICES masks can agree on different GPUs */
     _Atomic uint64_t arrive;        /* last agree sequence number this rank arrived at */
     _Atomic uint64_t ws_gen;        /* generation of the exported workspace */
     uint64_t ws_bytes;
@@ -109,8 +111,8 @@ typedef struct {
 /* Create (launcher / rank 0) or attach (others) the segment named `name`. */
 int ftar_ctrl_create(ftar_job *job, const char *name, int size);
 int ftar_ctrl_attach(ftar_job *job, const char *name, int rank, int size, int create_if_rank0);
-/* Claim this rank's slot: robust mutex locked, pid, state RUNNING. */
-int ftar_ctrl_join(ftar_job *job, int device);
+/* Claim this rank's slot: robust mutex locked, pid, device (ordinal + physical id), state RUNNING. */
+int ftar_ctrl_join(ftar_job *job, int device, const char *phys);
 void ftar_ctrl_leave(ftar_job *job);
 void ftar_ctrl_detach(ftar_job *job);
 

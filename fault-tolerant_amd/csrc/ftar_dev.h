@@ -66,6 +66,9 @@ int fdev_device_count(int *n);
 int fdev_open(int device, ftar_dev **out);
 void fdev_close(ftar_dev *d);
 int fdev_device(const ftar_dev *d);
+/* The device's physical identity (its PCI bus id, "dddd:bb:dd.f"): equal only for the same
+ * GPU, whatever HIP ordinal each process's visibility mask gives it. */
+int fdev_physical_id(ftar_dev *d, char *out, size_t n);
 
 int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle /* FDEV_HANDLE_BYTES */);
 /* blocks fdev_alloc_shared had to re-allocate because their IPC export was refused */

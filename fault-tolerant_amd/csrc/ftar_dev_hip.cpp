@@ -313,6 +313,13 @@ void fdev_close(ftar_dev *d)
 
 int fdev_device(const ftar_dev *d) { return d->device; }
 
+int fdev_physical_id(ftar_dev *d, char *out, size_t n)
+{
+    if (n < 16) return 13;
+    HIPCHK(hipDeviceGetPCIBusId(out, (int)n, d->device));
+    return 0;
+}
+
 // Round 1 saw one refused export (hipIpcGetMemHandle: invalid argument) when a sweep
 // re-allocated the workspace at every size, and round 2's 8-rank regrowth test saw it
 // once more, on a fresh 18 MiB block.  tools/ipc_probe.hip found no refusal in isolation;
@@ -493,7 +500,7 @@ static hipEvent_t get_event(ftar_dev *d)
 // launch gets such a marker on its own stream.
 static void note_launch(ftar_dev *d, hipStream_t st, unsigned grid, bool can_signal, ftar::KSignal *sig)
 {
-    if (sig) *sig = ftar::KSignal{nullptr, nullptr, 0, 0};
+    if (sig) *sig = ftar::KSignal{};
     // anything queued behind a closed gate would wait for it: the gated launch is given up
     // (opened as skip; it returns untouched) -- its caller finds the gate no longer pending
     if (d->gate_pending) (void)fdev_gate_open(d, 1);
@@ -502,7 +509,11 @@ static void note_launch(ftar_dev *d, hipStream_t st, unsigned grid, bool can_sig
         return;
     }
     if (can_signal && sig && d->flag_sync && grid <= d->flag_max) {
-        *sig = ftar::KSignal{d->sig_cnt, d->sig_flag, ++d->sig_tag, (unsigned)d->need_acquire};
+        *sig = ftar::KSignal{};
+        sig->cnt = d->sig_cnt;
+        sig->flag = d->sig_flag;
+        sig->tag = ++d->sig_tag;
+        sig->acquire = (unsigned)d->need_acquire;
         d->signalled++;
     } else {
         if (d->need_acquire) (void)hipEventRecord(d->fence_main, st);
@@ -651,8 +662,16 @@ static ftar::KSignal arm_gate(ftar_dev *d, double link, double hbm)
     __atomic_store_n(gate_err(d, d->gate_seq), 0u, __ATOMIC_RELAXED); // the slot's last gate was verified
     // the workgroups invalidate their caches once the gate opens (acquire = 1): whatever
     // the drains before it did, the peers' data is read fresh
-    return ftar::KSignal{d->sig_cnt, d->sig_flag, ++d->sig_tag, 1u, gate_word(d, d->gate_seq), 2u * d->gate_seq,
-                         gate_err(d, d->gate_seq), d->gate_ticks};
+    ftar::KSignal k{};
+    k.cnt = d->sig_cnt;
+    k.flag = d->sig_flag;
+    k.tag = ++d->sig_tag;
+    k.acquire = 1u;
+    k.gate = gate_word(d, d->gate_seq);
+    k.gate_val = 2u * d->gate_seq;
+    k.err = gate_err(d, d->gate_seq);
+    k.gate_ticks = d->gate_ticks;
+    return k;
 }
 
 // A short gated launch of several workgroups waits with ONE of them polling the host word
@@ -682,10 +701,10 @@ static void keep_plan(ftar_dev *d, int batch, int dtype, int op, int nsrc, unsig
     g.seq = d->gate_seq;
     if (batch) {
         g.B = *B;
-        g.B.sig = ftar::KSignal{nullptr, nullptr, 0, 0};
+        g.B.sig = ftar::KSignal{};
     } else {
         g.L = *L;
-        g.L.sig = ftar::KSignal{nullptr, nullptr, 0, 0};
+        g.L.sig = ftar::KSignal{};
     }
 }
 
@@ -1338,7 +1357,7 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
         return 0;
     }
     // MPI_Reduce_local(in, inout): inout = inout <op> in  -> x = inout, y = in
-    ftar::SegIn seg{ftar::kReduce, inout, inout, in, n, nullptr};
+    ftar::SegIn seg{ftar::kReduce, inout, inout, in, n, nullptr, 0};
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(&seg, 1, es, cached_blocks, &L);
     if (grid == 0) return 0;

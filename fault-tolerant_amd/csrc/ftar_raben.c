@@ -127,11 +127,11 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
         if (ag) { /* the last allgather step lands in rbuf: only there (fast_io) or also in W */
             int last = step == 0;
             pl[0] = (ftar_pull){FDEV_COPY, 0, src, WS_W, (x->fast_io && last) ? WS_UOUT : WS_W, WS_W, si[step],
-                                sc[step], !x->fast_io && last};
+                                sc[step], !x->fast_io && last, 0};
             P->npull[cr] = 1;
         } else if (step == 0) { /* fast_io: the local operand is sbuf itself */
-            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, x->fast_io ? WS_UIN : WS_IN, ri[0], rc[0], 0};
-            pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0], 0};
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, x->fast_io ? WS_UIN : WS_IN, ri[0], rc[0], 0, 0};
+            pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0], 0, 0};
             P->npull[cr] = x->keep_recov ? 2 : 1;
         } else {
             /* with an idle rank a partner's death mid-exchange is recoverable and the pulled
@@ -145,13 +145,13 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
 
 static void run_reduce(rb_ctx *x, void *out, const void *xin, const void *yin, int64_t n, int remote, int tag)
 {
-    fdev_seg s = {FDEV_REDUCE, remote, out, xin, yin, (size_t)n, NULL};
+    fdev_seg s = {FDEV_REDUCE, remote, out, xin, yin, (size_t)n, NULL, 0};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
 static void run_copy(rb_ctx *x, void *out, const void *src, int64_t n, int remote, int tag)
 {
-    fdev_seg s = {FDEV_COPY, remote, out, src, NULL, (size_t)n, NULL};
+    fdev_seg s = {FDEV_COPY, remote, out, src, NULL, (size_t)n, NULL, 0};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
@@ -339,7 +339,7 @@ static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf, void *rbuf)
         rb_windows(u, x->count, L, ri, si, rc, sc);
         void *R = ftar_buf(c, c->order[rb_real(x, u)], WS_R);
         segs[ns++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_OUT, rb_push_at(x, R, j, ri[L - 1]),
-                                at(x, (void *)sbuf, ri[L - 1]), NULL, (size_t)rc[L - 1], NULL};
+                                at(x, (void *)sbuf, ri[L - 1]), NULL, (size_t)rc[L - 1], NULL, 0};
     }
     double lb0 = ftar_link_bytes(c);
     ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP0);
@@ -404,7 +404,7 @@ static int rb_mesh_push_finish(rb_ctx *x, void *rbuf)
         int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
         rb_windows(v ^ j, x->count, L, ri, si, rc, sc);
         segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, ri[L - 1]), at(x, c->ws[WS_W], ri[L - 1]), NULL,
-                                (size_t)rc[L - 1], NULL};
+                                (size_t)rc[L - 1], NULL, 0};
     }
     ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_LOCAL);
     ftar_drain(c);
@@ -445,14 +445,14 @@ static int rb_mesh_ag_segs(rb_ctx *x, void *rbuf, fdev_seg *segs)
     const int L = x->steps, p = x->adjsize, v = x->vrank;
     int ns = 0;
     segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, x->rindex[L - 1]), at(x, c->ws[WS_W], x->rindex[L - 1]), NULL,
-                            (size_t)x->rcount[L - 1], NULL};
+                            (size_t)x->rcount[L - 1], NULL, 0};
     for (int j = 1; j < p; j++) {
         int u = v ^ j;
         int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
         rb_windows(u, x->count, L, ri, si, rc, sc);
         void *PW = ftar_buf(c, c->order[rb_real(x, u)], WS_W);
         segs[ns++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, rbuf, ri[L - 1]), at(x, PW, ri[L - 1]), NULL,
-                                (size_t)rc[L - 1], NULL};
+                                (size_t)rc[L - 1], NULL, 0};
     }
     return ns;
 }
@@ -753,9 +753,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     } else if (x->mesh) { /* peers pull every block of sbuf but this rank's own final one */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         int64_t b0 = x->rindex[x->steps - 1], b1 = b0 + x->rcount[x->steps - 1];
-        fdev_seg cp[2] = {{FDEV_COPY, 0, IN, sbuf, NULL, (size_t)b0, NULL},
+        fdev_seg cp[2] = {{FDEV_COPY, 0, IN, sbuf, NULL, (size_t)b0, NULL, 0},
                           {FDEV_COPY, 0, at(x, IN, b1), at(x, (void *)sbuf, b1), NULL, (size_t)((int64_t)count - b1),
-                           NULL}};
+                           NULL, 0}};
         ftar_run(c, x->dtype, x->op, cp, 2, FDEV_TAG_LOCAL);
     } else if (x->fast_io) { /* the half of sbuf peers pull at step 0 */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
@@ -852,9 +852,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                 void *PIN = ftar_buf(c, pl[0].src, WS_IN);
                 fdev_seg red = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, pl[0].off),
                                 at(x, ftar_local(c, pl[0].x_buf), pl[0].off), at(x, PIN, pl[0].off), (size_t)pl[0].n,
-                                NULL};
+                                NULL, 0};
                 fdev_seg cpy = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
-                                (size_t)pl[1].n, NULL};
+                                (size_t)pl[1].n, NULL, 0};
                 ftar_run_pulls(c, x->dtype, x->op, &red, 1, FDEV_TAG_STEP0, 0);
                 if (x->keep_recov) {
                     ftar_run_pulls(c, x->dtype, x->op, &cpy, 1, FDEV_TAG_BG, 1);
@@ -900,7 +900,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             c->stats.steps++;
         }
         /* last step: this rank's own final half W -> rbuf rides in the same launch */
-        fdev_seg own = {FDEV_COPY, 0, NULL, NULL, NULL, 0, NULL};
+        fdev_seg own = {FDEV_COPY, 0, NULL, NULL, NULL, 0, NULL, 0};
         int nown = 0;
         if (step == 0 && x->vrank != -1) {
             own.out = at(x, rbuf, x->rindex[0]);

@@ -56,7 +56,7 @@ static int peer_cur(rd_ctx *x, int w) { return (int)ftar_peer_pub(x->c, w); }
 
 static void run1(rd_ctx *x, int kind, void *out, const void *a, const void *b, int remote, int tag)
 {
-    fdev_seg s = {kind, remote, out, a, b, x->count, NULL};
+    fdev_seg s = {kind, remote, out, a, b, x->count, NULL, 0};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
@@ -77,7 +77,7 @@ static int rd_plan(rd_ctx *x, int distance, int cur, int pred, ftar_plan *P)
         int cr = ftar_comm_rank_of(c, x->active[a]);
         int pw = x->active[a ^ distance];
         ftar_pull *pl = &P->pull[cr][0];
-        *pl = (ftar_pull){FDEV_REDUCE, last, pw, pred >= 0 ? pred : peer_cur(x, pw), 0, 0, 0, (int64_t)x->count, 0};
+        *pl = (ftar_pull){FDEV_REDUCE, last, pw, pred >= 0 ? pred : peer_cur(x, pw), 0, 0, 0, (int64_t)x->count, 0, 0};
         if (a == i) {
             pl->dst_buf = out;
             pl->x_buf = cur;

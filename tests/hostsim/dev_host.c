@@ -97,6 +97,27 @@ int fdev_gate_relaunches(const ftar_dev *d) { return 0; }
 void fdev_close(ftar_dev *d) { free(d); }
 int fdev_device(const ftar_dev *d) { return d->device; }
 
+/* "hostsim:<ordinal>", or the FTAR_RANK-th entry of FTAR_HOSTSIM_PHYS (comma list): the
+ * case of ranks that see different GPUs under one ordinal (per-rank visibility masks) */
+int fdev_physical_id(ftar_dev *d, char *out, size_t n)
+{
+    const char *l = getenv("FTAR_HOSTSIM_PHYS"), *r = getenv("FTAR_RANK");
+    if (l && r) {
+        int k = atoi(r);
+        while (k-- > 0 && l) {
+            l = strchr(l, ',');
+            if (l) l++;
+        }
+        if (l) {
+            size_t m = strcspn(l, ",");
+            snprintf(out, n, "%.*s", (int)m, l);
+            return 0;
+        }
+    }
+    snprintf(out, n, "hostsim:%d", d->device);
+    return 0;
+}
+
 static int put_map(void *p, size_t n, const char *name, int own)
 {
     for (int i = 0; i < MAXMAP; i++)

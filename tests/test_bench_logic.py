@@ -270,6 +270,47 @@ def test_north_star_block_prices():
     assert reh["frac"] is None and reh["met"] is None and reh["rehearsal"]
 
 
+def test_rd_roofline_and_non_kernel_time():
+    """configs[2] (RD, 256 MiB, 8 GPUs) gets a link roofline on the node
+    line, and the headline's north-star block carries the call's time outside kernels.  A
+    synthetic node line: RD relayed in 3.2 ms (its own bound: 3 steps x 2 S / 8 over each of
+    7 links = 2.62 ms at 76.8 GB/s), the direct transport -- the reference's movement, L S
+    over one link per step, 10.49 ms -- in 11.5 ms; the mesh headline 1.3 ms of which 1.0 ms
+    kernels."""
+    m = _bench_module()
+    S = 256 << 20
+    rd = m.rd_roofline_block(8, S, 3.2e-3, "relay2hop", 76.8, t_direct=11.5e-3,
+                             breakdown={"call_ms": 3.3, "kernels_ms": 2.9})
+    t_own = 3 * 2.0 * S / 8 / 76.8e9
+    t_ref = 3.0 * S / 76.8e9
+    assert rd["links"] == 7 and rd["schedule_bytes_per_link"] == 3 * 2.0 * S / 8
+    assert rd["frac"] == round(t_own / 3.2e-3, 4) and rd["frac"] <= 1.0
+    assert rd["reference_schedule_frac"] == round(t_ref / 11.5e-3, 4) <= 1.0
+    assert rd["speedup_vs_reference_roofline"] == round(t_ref / 3.2e-3, 4) > 1  # a speed-up, not a fraction
+    assert abs(rd["non_kernel_ms"] - 0.4) < 1e-9 and rd["kernels_ms"] == 2.9
+    assert all(f is None or f <= 1.0 for f in _fracs(rd)), _fracs(rd)
+    # direct: the reference's own data movement, one link per step
+    d = m.rd_roofline_block(8, S, 11.5e-3, "direct", 76.8, t_direct=11.5e-3)
+    assert d["links"] == 1 and d["frac"] == d["reference_schedule_frac"] == round(t_ref / 11.5e-3, 4)
+    # p = 9 (a spare): the pre-step and the fan-out each move one more vector on the path
+    d9 = m.rd_roofline_block(9, S, 20e-3, "direct", 76.8)
+    assert d9["reference_bytes_per_rank"] == 5.0 * S
+    # a time below the bound claims no fraction above 1
+    fast = m.rd_roofline_block(8, S, 2.0e-3, "relay2hop", 76.8)
+    assert fast["frac"] is None and "bound_violated" in fast
+    # one-GPU rehearsal: printed, fractions withheld
+    reh = m.rd_roofline_block(2, S, 1e-3, "direct", None, t_direct=1e-3, rehearsal=True)
+    assert reh["frac"] is None and reh["reference_schedule_frac"] is None
+    # the north-star block: time outside kernels beside the fraction
+    ns = m.north_star_block(8, S, 1.3e-3, "mesh", 76.8, 7, 2.0 * S / 8,
+                            breakdown={"call_ms": 1.3, "kernels_ms": 1.0, "agree_barrier_wait_ms": 0.2,
+                                       "stream_drain_wait_ms": 0.1})
+    assert abs(ns["non_kernel_ms"] - 0.3) < 1e-9 and ns["kernels_ms"] == 1.0
+    assert ns["non_kernel_share"] == round(0.3 / 1.3, 4)
+    assert ns["frac_kernels_only"] == round(2.0 * S / 8 / 76.8e9 / 1.0e-3, 4) <= 1.0
+    assert all(f is None or f <= 1.0 for f in _fracs(ns)), _fracs(ns)
+
+
 def _torchrun_cpu(tmp_path, extra_env, extra_args, timeout):
     import socket
     import subprocess
@@ -316,6 +357,7 @@ def test_bench_multi_headline_survives_hung_and_failing_legs(hostsim, tmp_path):
     assert fin["transports"]["direct"]["error"].startswith("transports:direct: forced failure")
     assert fin["transports"]["relay2hop"]["raben_ms"] > 0
     assert fin["legs"]["rd"]["status"] == "error" and fin["rd"] is None
+    assert "non_kernel_ms" in fin["north_star"] and fin["north_star"]["kernels_ms"] >= 0
     assert fin["exact_on_node"]["all_exact"], fin["exact_on_node"]
     assert fin["int32_rank_checksum_ok"] == {"raben": True, "rd": True}
     assert fin["cpu_baseline"]["value"] and fin["cpu_baseline"]["cores"] == 2
@@ -357,6 +399,10 @@ def test_bench_multi_small_call_fallback(hostsim, tmp_path):
     sweep = fin["size_sweep_us"]
     assert sweep["small_call_setting"] == "gate=0" and sweep["gate"] == 0, sweep
     assert fin["transport_selection"]["inexact"], fin["transport_selection"]  # the gated one-shot failed there too
+    # configs[2]'s roofline block rides on the RD leg (fractions withheld off the node)
+    rl = fin["rd"]["schedule_link_roofline"]
+    assert rl["transport"] == "direct" and rl["links"] == 1 and rl["frac"] is None and rl["rehearsal"], rl
+    assert rl["reference_bytes_per_rank"] == 4.0 * 65536 and "non_kernel_ms" in rl, rl
 
 
 @pytest.mark.timeout(240)

@@ -912,3 +912,29 @@ def test_redundancy_auto_follows_the_devmap(hostsim, oracle, p):
     # power of two (no spare): no handler can use the copy, whatever the layout
     r = H.run_probe("raben", ins[:4], backend="hostsim", devmap="0,1,2,3")
     assert all(r.status[w][0][12] == 0 for w in range(4)), r.status
+
+
+def test_redundancy_auto_uses_physical_device_ids(hostsim, oracle):
+    """under per-rank HIP_VISIBLE_DEVICES masks every rank may see its own GPU as
+    ordinal 0.  The auto redundancy decision compares the physical identities the ranks
+    publish (PCI bus ids; FTAR_HOSTSIM_PHYS stands in for them here), not the ordinals: one
+    ordinal on two physical GPUs moves the step-0 copy, and a replaying kill recovers bit-exact
+    with the victim's input withdrawn; one physical GPU under every ordinal elides it."""
+    p = 5
+    ins = oracle.random_inputs(p, 257, seed=41)
+    one_ordinal = ",".join("0" for _ in range(p))
+    two_phys = ",".join(f"0000:{5 + r % 2:02x}:00.0" for r in range(p))
+    r = H.run_probe("raben", ins, backend="hostsim", devmap=one_ordinal, env_extra={"FTAR_HOSTSIM_PHYS": two_phys})
+    assert all(r.status[w][0][12] == 1 for w in range(p)), r.status  # the copy moved
+    same_phys = ",".join("0000:05:00.0" for _ in range(p))
+    r = H.run_probe("raben", ins, backend="hostsim", devmap="0,1,0,1,0", env_extra={"FTAR_HOSTSIM_PHYS": same_phys})
+    assert all(r.status[w][0][12] == 0 for w in range(p)), r.status  # one physical GPU: elided
+    ks = [(3, 1, 1, 3)]
+    o = oracle.rabenseifner(ins, ks)
+    assert not o.aborted and o.status[3] == oracle.DEAD
+    r = H.run_probe("raben", ins, ks, backend="hostsim", devmap=one_ordinal,
+                    env_extra={"FTAR_HOSTSIM_PHYS": two_phys, "FTAR_KILL_WITHDRAW": "1"})
+    assert not r.aborted, r.stderr[-800:]
+    for w, s in enumerate(o.status):
+        if s == 0:
+            assert np.array_equal(r.outputs[w][0].view(np.uint32), o.outputs[w].view(np.uint32)), w

@@ -69,7 +69,7 @@ def main():
             comm.set_option(ftar.OPT_GATE_MAX, 16 << 20 if gate else 1 << 20)
             for _ in range(5):
                 assert fn(x, y) == 0
-            wall, drain, sync, kern, cwall, gated = [], [], [], [], [], []
+            wall, drain, sync, kern, cwall, gated, holds = [], [], [], [], [], [], []
             for _ in range(iters):
                 comm.barrier()
                 t0 = time.perf_counter()
@@ -81,11 +81,15 @@ def main():
                 kern.append(st.step0_kernel_ms * 1e-3)
                 cwall.append(st.wall_s)
                 gated.append(st.gated_launches - st.gated_skips)
+                holds.append(st.gate_holds)
             key = name + ("_profiled" if prof else "")
             # wall: the Python call; c_wall: inside the C entry point (ftar_stats wall_s,
             # what a C caller of include/ftar.h pays, minus the argument checks)
             res[key] = {"wall_us": med(wall), "c_wall_us": med(cwall), "drain_us": med(drain),
-                        "sync_wait_us": med(sync), "gated_calls": sum(1 for g in gated if g)}
+                        "sync_wait_us": med(sync), "gated_calls": sum(1 for g in gated if g),
+                        # gated launches given up at a barrier that waited past FTAR_GATE_HOLD_US: a
+                        # row where most are given up measures the hold, not the gate
+                        "gate_holds": sum(holds)}
             if prof:
                 res[key]["step0_kernel_us"] = med(kern)
     comm.set_option(ftar.OPT_ONESHOT_MAX, 1 << 20)
