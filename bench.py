@@ -949,9 +949,14 @@ def multi(args):
         the dominant kernel's device time from a shorter profiled pass."""
         comm.set_profiling(False)
         t, _ = timed(fn)
+        plain = timed.breakdown
         comm.set_profiling(True)
         _, k = timed(fn, max(3, args.steps // 4), 1)
-        timed_split.breakdown = dict(timed.breakdown, profiled=True)
+        # the split of the profiled pass (kernel events on: nothing is gated there), with the
+        # plain pass's call time and gate counts beside it
+        timed_split.breakdown = dict(timed.breakdown, profiled=True, plain_call_ms=plain["call_ms"],
+                                     plain_gated_launches=plain["gated_launches"],
+                                     plain_gate_holds=plain["gate_holds"])
         return t, k
 
     class CallFailed(RuntimeError):
@@ -974,6 +979,7 @@ def multi(args):
             ftar.OPT_TREE_UNROLL)
     pads = (0, 0, 0, 0, 0, 0, 1)  # PUSH off and one vector per tree lane unless named
     defaults = {o: comm.get_option(o) for o in opts}
+    gmax_lib = comm.get_option(ftar.OPT_GATE_MAX)  # the library's mid-size gate limit (1 MiB)
 
     def set_opts(vals):
         vals = tuple(vals) + pads[len(vals):]
@@ -1021,21 +1027,29 @@ def multi(args):
         # which one the fabric moves faster is measured here, not assumed
         # (mesh, relay, push, tree unroll)
         cands = {}
+        g0 = gmax_lib
         if pow2 and comm.get_option(ftar.OPT_MESH):
-            cands["mesh"] = (1, 1, 0, 1)
+            cands["mesh"] = (1, 1, 0, 1, g0)
             if world in (4, 8):
                 # 2 / 4 vectors per lane and source in the tree kernel: more loads in flight
                 # per lane when the p - 1 sources are remote (xGMI latency) -- the one-GPU A/B
                 # saw HBM contention only, so the node decides
-                cands["mesh_u2"] = (1, 1, 0, 2)
-                cands["mesh_u4"] = (1, 1, 0, 4)
-            cands["mesh_push"] = (1, 1, 1, 1)  # remote stores in the reduce-scatter
+                cands["mesh_u2"] = (1, 1, 0, 2, g0)
+                cands["mesh_u4"] = (1, 1, 0, 4, g0)
+            cands["mesh_push"] = (1, 1, 1, 1, g0)  # remote stores in the reduce-scatter
             if world <= 8:
-                cands["mesh_push2"] = (1, 1, 2, 1)  # ... and in the allgather
+                cands["mesh_push2"] = (1, 1, 2, 1, g0)  # ... and in the allgather
+            if world > 2 and comm.get_option(ftar.OPT_GATE):
+                # the allgather's launch queued behind the tree at this size too (FTAR_OPT_GATE_MAX
+                # >= S), its gate opened by the reduce-scatter's agree: the launch latency after
+                # the barrier leaves the call's non-kernel time.  On one
+                # GPU shared by the ranks the waiting launch holds CUs the others need (DESIGN.md
+                # 6); with one rank per GPU nothing else competes -- the node decides
+                cands["mesh_gated_ag"] = (1, 1, 0, 1, max(float(S), g0))
         if world >= 3 and comm.get_option(ftar.OPT_RELAY):
-            cands["relay2hop"] = (0, 1, 0, 1)
-        cands["direct"] = (0, 0, 0, 1)
-        sel_opts = (ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH, ftar.OPT_TREE_UNROLL)
+            cands["relay2hop"] = (0, 1, 0, 1, g0)
+        cands["direct"] = (0, 0, 0, 1, g0)
+        sel_opts = (ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH, ftar.OPT_TREE_UNROLL, ftar.OPT_GATE_MAX)
         if len(cands) > 1:
             times, inexact, failed = {}, [], {}
             for name, vals in cands.items():
@@ -1056,7 +1070,7 @@ def multi(args):
             else:  # every one failed: keep the defaults, exact_on_node reports it
                 chosen = None
                 for o in sel_opts:
-                    comm.set_option(o, defaults[o])
+                    comm.set_option(o, defaults[o] if o in defaults else gmax_lib)
             selection = {f"{k}_ms": round(t * 1e3, 4) for k, t in times.items()}
             selection.update({"chosen": chosen, "inexact": inexact, "failed": failed})
 
@@ -1070,10 +1084,18 @@ def multi(args):
     push_opt = int(comm.get_option(ftar.OPT_PUSH))
     pushed = meshed and not oneshot and push_opt != 0
     unroll = int(comm.get_option(ftar.OPT_TREE_UNROLL)) if world in (4, 8) else 1
+    # the headline's allgather queued behind the tree (mesh_gated_ag): counted in the plain pass
+    # (the profiled pass gates nothing: kernel events would time the wait)
+    gated_ag = meshed and not oneshot and not pushed and breakdown.get("plain_gated_launches", 0) > 0
     transport = "mesh-oneshot" if oneshot else ("mesh-push2" if push_opt == 2 and world <= 8 else "mesh-push") \
-        if pushed else (f"mesh-u{unroll}" if unroll > 1 else "mesh") if meshed else "relay2hop" if relayed else "direct"
+        if pushed else "mesh-gated-ag" if gated_ag else (f"mesh-u{unroll}" if unroll > 1 else "mesh") if meshed \
+        else "relay2hop" if relayed else "direct"
     keep = bool(comm.last_stats().step0_copy)  # the headline call moved the reference's step-0 copy
     chosen_opts = {o: comm.get_option(o) for o in opts}
+    # the headline's gate limit (S when mesh_gated_ag was chosen); every later leg runs at the
+    # library's default unless it names its own
+    head_gate_max = comm.get_option(ftar.OPT_GATE_MAX)
+    comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)
 
     L = world.bit_length() - 1
     r_core = 1 << L  # ranks in the power-of-two core: the receivers of every exchange step
@@ -1131,6 +1153,8 @@ def multi(args):
                    "flight), allgather as one multi-source pull (power-of-two p, no spare; same tree)",
         "mesh-u4": "Rabenseifner, one-hop mesh, tree kernel with 4 vectors per lane and source (more remote loads in "
                    "flight), allgather as one multi-source pull (power-of-two p, no spare; same tree)",
+        "mesh-gated-ag": "Rabenseifner, one-hop mesh, the allgather's multi-source pull queued behind the tree kernel "
+                         "and opened by the reduce-scatter's agree (FTAR_OPT_GATE_MAX >= S; power-of-two p, no spare)",
         "mesh-push": "Rabenseifner, one-hop mesh, push form: every rank stores its part of each block into the "
                      "owner's HBM (p-1 remote-store copies in one launch), each owner reduces its block locally in the "
                      "same tree, allgather as one multi-source pull (power-of-two p, no spare)",
@@ -1276,7 +1300,7 @@ def multi(args):
         base = [chosen_opts[o] for o in opts]
         raben_fn, rd_fn = comm.allreduce_rabenseifner, comm.recursive_doubling
         # (name, option values, function, count or None = the job's, extra options)
-        checks = [("chosen", base, raben_fn, None, {}),
+        checks = [("chosen", base, raben_fn, None, {ftar.OPT_GATE_MAX: head_gate_max}),
                   ("reference_shape", (0, 0, 0, 1, 0), raben_fn, None, {}),
                   ("rd", base, rd_fn, None, {}),
                   ("chosen_64KiB", base, raben_fn, 16384, {})]
@@ -1297,6 +1321,11 @@ def multi(args):
                         ("mesh_push", (1, 1, 0, 0, 1, 1)), ("mesh_push2", (1, 1, 0, 0, 1, 2)),
                         ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)))
                        if pow2 or not name.startswith("mesh")]
+            if pow2 and world > 2:
+                # the allgather queued behind the tree at the job's size (transport selection's
+                # mesh_gated_ag)
+                checks.append(("mesh_gated_ag", (1, 1, 0, 0, 1), raben_fn, None,
+                               {ftar.OPT_GATE_MAX: max(float(S), gmax_lib)}))
             if pow2:
                 checks += [(name, vals, raben_fn, min(16384, args.count), {}) for name, vals in
                            (("mesh_push_64KiB", (1, 1, 0, 0, 1, 1)), ("mesh_push2_64KiB", (1, 1, 0, 0, 1, 2)),
@@ -1407,7 +1436,8 @@ def multi(args):
         # the partner's window + a local reduce kernel; relay_full_exchange: the relay with
         # the reference's step-0 full exchange.  Each variant records its own failure.
         out = {}
-        variants = (("mesh", (1, 1, 0, 0, 1)), ("mesh_push", (1, 1, 0, 0, 1, 1)), ("mesh_push2", (1, 1, 0, 0, 1, 2)),
+        variants = (("mesh", (1, 1, 0, 0, 1)), ("mesh_gated_ag", (1, 1, 0, 0, 1)),
+                    ("mesh_push", (1, 1, 0, 0, 1, 1)), ("mesh_push2", (1, 1, 0, 0, 1, 2)),
                     ("relay2hop", (1, 1, 0, 0, 0)),
                     ("direct", (0, 1, 0, 0, 0)), ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
                     ("relay_full_exchange", (1, 1, 0, 1, 0)))
@@ -1418,10 +1448,15 @@ def multi(args):
                 if time_left() < 10:
                     out[name] = {"skipped": "budget"}
                     continue
+                if name == "mesh_gated_ag" and (world == 2 or not comm.get_option(ftar.OPT_GATE)):
+                    continue
                 try:
                     maybe_fail(f"transports:{name}")
                     set_opts(vals)
+                    if name == "mesh_gated_ag":
+                        comm.set_option(ftar.OPT_GATE_MAX, max(float(S), gmax_lib))
                     tv, kv = timed_split(raben)
+                    comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)
                     lb = timed.link_bytes
                     tv_rd = timed(rd)[0] if name in ("relay2hop", "direct", "copy_engine") else None
                     out[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2),
@@ -1429,10 +1464,14 @@ def multi(args):
                                  "step0_pull_GBps": round(lb / (kv * 1e-3) / 1e9, 2) if kv > 0 else None}
                     if tv_rd:
                         out[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
+                    if name == "mesh_gated_ag":
+                        out[name]["plain_gated_launches"] = timed_split.breakdown.get("plain_gated_launches")
+                        out[name]["plain_gate_holds"] = timed_split.breakdown.get("plain_gate_holds")
                 except Exception as e:
                     out[name] = {"error": str(e)[-300:]}
         finally:
             set_opts([chosen_opts[o] for o in opts])
+            comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)
         return out
 
     def sweep_leg():

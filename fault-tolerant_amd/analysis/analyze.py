@@ -260,6 +260,9 @@ def decisions(line: dict) -> dict:
         "transport_ms": times,
         "transport_inexact_or_failed": sorted(set(sel.get("inexact") or []) | set(sel.get("failed") or {})),
         "never_fastest": sorted(k for k in times if k != sel.get("chosen")),
+        # the allgather queued behind the tree at the headline size
+        "gated_ag_faster": (times["mesh_gated_ag"] < times["mesh"]) if "mesh_gated_ag" in times and "mesh" in times
+        else None,
         "gate_max_bytes": gate_max,
         "gate_max_changes": gate_max != (1 << 20),
         "all_exact": ex.get("all_exact"),

@@ -311,7 +311,7 @@ def test_rd_roofline_and_non_kernel_time():
     assert all(f is None or f <= 1.0 for f in _fracs(ns)), _fracs(ns)
 
 
-def _torchrun_cpu(tmp_path, extra_env, extra_args, timeout):
+def _torchrun_cpu(tmp_path, extra_env, extra_args, timeout, nproc=2, count=65536):
     import socket
     import subprocess
     import sys
@@ -322,9 +322,9 @@ def _torchrun_cpu(tmp_path, extra_env, extra_args, timeout):
     env = dict(os.environ, FTAR_BENCH_CPU_TEST="1", FTAR_HOSTSIM_TAG=f"bench{os.getpid()}", **extra_env)
     for k in ("FTAR_JOB", "FTAR_RANK", "FTAR_SIZE", "FTAR_LAUNCHER", "FTAR_KILL", "FTAR_DEVICE"):
         env.pop(k, None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
-           "--dist-backend", "gloo", "--count", "65536", "--steps", "3", "--warmup", "1"] + extra_args
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--device",
+           "cpu", "--dist-backend", "gloo", "--count", str(count), "--steps", "3", "--warmup", "1"] + extra_args
     t0 = time.monotonic()
     cp = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
     subprocess.run(f"rm -f /dev/shm/ftarhs-bench{os.getpid()}-*", shell=True)
@@ -415,3 +415,25 @@ def test_bench_multi_watchdog_prints_and_exits(hostsim, tmp_path):
     assert [d["line"] for d in lines] == ["headline", "final"], cp.stdout[-2000:]
     assert "watchdog" in lines[-1]["truncated"] and lines[-1]["value"] == lines[0]["value"]
     assert took < 30 + 30, took
+
+
+@pytest.mark.timeout(240)
+def test_bench_multi_four_ranks_gated_allgather(hostsim, tmp_path):
+    """Four ranks, 4 MiB per rank (above the one-shot and gate limits): the transport
+    selection times `mesh_gated_ag` -- the mesh with its allgather queued behind the tree
+    (FTAR_OPT_GATE_MAX >= S) -- beside the others, exact_on_node checks it at the job's size,
+    the transports leg reports its gated launches, node_decisions says whether it was faster,
+    and configs[2]'s roofline block carries L = 2 steps of the reference's movement."""
+    cp, lines, took = _torchrun_cpu(tmp_path, {}, ["--side-budget", "5", "--no-c5", "--no-xgmi", "--no-cpu-baseline"],
+                                    200, nproc=4, count=1 << 20)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    fin = lines[-1]
+    sel = fin["transport_selection"]
+    assert "mesh_gated_ag_ms" in sel and "mesh_ms" in sel and not sel["inexact"] and not sel["failed"], sel
+    assert fin["exact_on_node"]["mesh_gated_ag"] and fin["exact_on_node"]["all_exact"], fin["exact_on_node"]
+    assert fin["transports"]["mesh_gated_ag"]["plain_gated_launches"] > 0, fin["transports"]["mesh_gated_ag"]
+    nd = fin["node_decisions"]
+    assert nd["gated_ag_faster"] in (True, False), nd
+    rl = fin["rd"]["schedule_link_roofline"]
+    assert rl["reference_bytes_per_rank"] == 2.0 * 4 * (1 << 20), rl
+    assert "non_kernel_ms" in fin["north_star"], fin["north_star"]

@@ -539,6 +539,31 @@ def test_gated_launches_mid_size(hostsim, oracle, algo, p):
     assert r.returncode == 0 and all(r.status[w][0][10] == 0 for w in range(p)), r.status
 
 
+@pytest.mark.timeout(300)
+def test_gated_allgather_at_the_headline_size(hostsim):
+    """VERDICT r04 next #3 (`mesh_gated_ag`, bench.py's transport selection): with
+    FTAR_GATE_MAX >= S the mesh queues its allgather launch behind the tree at the headline
+    size too (256 MiB float32-sized vectors, here int32 so the sum is exact in any order), and
+    the reduce-scatter's agree opens it: exactly one gated launch per call, never replaced,
+    the result exact; at the default limit nothing is gated."""
+    p, n = 4, 1 << 26
+    rng = np.random.default_rng(11)
+    ins = [rng.integers(-1 << 20, 1 << 20, n, dtype=np.int32) for _ in range(p)]
+    want = np.sum(np.stack(ins), axis=0, dtype=np.int64).astype(np.int32)
+    env = {"FTAR_GATE_HOLD_US": "0", "FTAR_PROBE_DEVICE": "1", "FTAR_MESH": "1", "FTAR_PUSH": "0",
+           "FTAR_GATE_MAX": str(4 * n)}
+    r = H.run_probe("raben", ins, iters=2, backend="hostsim", env_extra=env, timeout=280)
+    assert r.returncode == 0, r.stderr[-1000:]
+    for w in range(p):
+        for it in range(2):
+            assert r.status[w][it][9] == 2, r.status[w][it]  # the two-launch mesh
+            assert r.status[w][it][10:12] == (1, 0), (w, it, r.status[w][it])
+            assert np.array_equal(r.outputs[w][it], want), (w, it)
+    r = H.run_probe("raben", ins[:p], backend="hostsim", env_extra=dict(env, FTAR_GATE_MAX=str(1 << 20)),
+                    timeout=280)
+    assert r.returncode == 0 and all(r.status[w][0][10] == 0 for w in range(p)), r.status
+
+
 @pytest.mark.parametrize("algo", ["raben", "rd"])
 @pytest.mark.parametrize("p", [2, 4])
 def test_gated_launch_replaced_when_a_peer_reads_in_place(hostsim, oracle, algo, p):
