@@ -195,6 +195,12 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
         free(c);
         return rc;
     }
+    const char *tp = getenv("FTAR_TRACE"); /* test instrumentation: tests/fence_check.py */
+    if (tp && *tp) {
+        char path[512];
+        snprintf(path, sizeof(path), "%s.%d", tp, rank);
+        if (fdev_trace_open(c->dev, path)) fprintf(stderr, "ftar: rank %d: %s\n", rank, fdev_last_error());
+    }
     c->size = size;
     for (int i = 0; i < size; i++) c->order[i] = i;
     recompute_members(c);
@@ -240,11 +246,14 @@ int ftar_init(ftar_comm **out)
     return ftar_init_rank(out, name, rank, size, device);
 }
 
+static const char *const ws_name[FTAR_NBUF] = {"IN", "W", "T", "R"};
+
 static void release_peers(ftar_comm *c)
 {
     for (int w = 0; w < c->wsize; w++)
         for (int b = 0; b < FTAR_NBUF; b++)
             if (c->peer[w][b]) {
+                fdev_trace_unregion(c->dev, c->peer[w][b]);
                 fdev_unimport(c->dev, c->peer[w][b]);
                 c->peer[w][b] = NULL;
             }
@@ -255,6 +264,7 @@ static void release_user_peers(ftar_comm *c)
     for (int w = 0; w < c->wsize; w++)
         for (int k = 0; k < FTAR_UCACHE; k++)
             if (c->ucache[w][k].base) {
+                fdev_trace_unregion(c->dev, c->ucache[w][k].base);
                 fdev_unimport(c->dev, c->ucache[w][k].base);
                 c->ucache[w][k].base = NULL;
                 c->ucache[w][k].id = 0;
@@ -275,6 +285,10 @@ int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
     me->uoff = off;
     me->useq = (uint64_t)c->ncalls; /* a rank that dies before this point leaves an older tag */
     if (ok) {
+        char nm[32];
+        snprintf(nm, sizeof(nm), "U%llu", (unsigned long long)id);
+        fdev_trace_region(c->dev, (const char *)sbuf - off, off + bytes, c->wrank, nm);
+        fdev_trace_external_write(c->dev, sbuf, bytes); /* the caller wrote it: needs the fenced drain */
         c->in_alias = sbuf;
         /* peers read the caller's memory in place: the drain before the call's first barrier
          * must write it back device-wide (a fenced marker), whatever this rank launched */
@@ -294,11 +308,17 @@ static void *peer_sbuf(ftar_comm *c, int w, int *failed)
     for (int k = 0; k < FTAR_UCACHE; k++) {
         if (c->ucache[w][k].base && c->ucache[w][k].id == id) {
             c->ucache[w][k].used = ++c->ucache_clock;
+            char nm[32];
+            snprintf(nm, sizeof(nm), "U%llu", (unsigned long long)id);
+            fdev_trace_region(c->dev, c->ucache[w][k].base, s->uoff + c->in_bytes, w, nm);
             return (char *)c->ucache[w][k].base + s->uoff;
         }
         if (c->ucache[w][k].used < c->ucache[w][victim].used) victim = k;
     }
-    if (c->ucache[w][victim].base) fdev_unimport(c->dev, c->ucache[w][victim].base);
+    if (c->ucache[w][victim].base) {
+        fdev_trace_unregion(c->dev, c->ucache[w][victim].base);
+        fdev_unimport(c->dev, c->ucache[w][victim].base);
+    }
     c->ucache[w][victim].base = NULL;
     c->ucache[w][victim].id = 0;
     void *base = NULL;
@@ -309,6 +329,9 @@ static void *peer_sbuf(ftar_comm *c, int w, int *failed)
     c->ucache[w][victim].id = id;
     c->ucache[w][victim].base = base;
     c->ucache[w][victim].used = ++c->ucache_clock;
+    char nm[32];
+    snprintf(nm, sizeof(nm), "U%llu", (unsigned long long)id);
+    fdev_trace_region(c->dev, base, s->uoff + c->in_bytes, w, nm);
     return (char *)base + s->uoff;
 }
 
@@ -553,7 +576,9 @@ uint64_t ftar_sync(ftar_comm *c)
         c->job.wait_arg = c;
         c->job.wait_after_s = c->gate_hold_s;
     }
+    fdev_trace_note(c->dev, "A %llu", (unsigned long long)next);
     uint64_t snap = ftar_ctrl_agree(&c->job, c->members);
+    fdev_trace_note(c->dev, "P %llu", (unsigned long long)c->job.seq);
     c->job.wait_hook = NULL;
     double dt = now_s() - t0;
     c->stats.sync_wait_s += dt;
@@ -820,6 +845,7 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
                     fdev_last_error());
             ftar_ctrl_abort(&c->job, FTAR_ERR_NOMEM);
         }
+        fdev_trace_region(c->dev, c->ws[b], nb, c->wrank, ws_name[b]);
     }
     me->ws_bytes = nb;
     atomic_fetch_add(&me->ws_gen, 1);
@@ -836,15 +862,22 @@ int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
                         fdev_last_error());
                 ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
             }
+            fdev_trace_region(c->dev, c->peer[w][b], s->ws_bytes, w, ws_name[b]);
         }
         c->peer_bytes[w] = s->ws_bytes;
         c->peer_gen[w] = atomic_load(&s->ws_gen);
     }
     for (int w = 0; w < c->wsize; w++) /* the old mappings, dead ranks' included */
         for (int b = 0; b < FTAR_NBUF; b++)
-            if (old_peer[w][b]) fdev_unimport(c->dev, old_peer[w][b]);
+            if (old_peer[w][b]) {
+                fdev_trace_unregion(c->dev, old_peer[w][b]);
+                fdev_unimport(c->dev, old_peer[w][b]);
+            }
     ftar_sync_fatal(c); /* nobody maps the old buffers */
-    for (int b = 0; b < FTAR_NBUF; b++) fdev_free(c->dev, old_ws[b]);
+    for (int b = 0; b < FTAR_NBUF; b++) {
+        fdev_trace_unregion(c->dev, old_ws[b]);
+        fdev_free(c->dev, old_ws[b]);
+    }
     return FTAR_SUCCESS;
 }
 

@@ -184,6 +184,18 @@ void fdev_profiling(ftar_dev *d, int on);
 void fdev_counters_reset(ftar_dev *d);
 void fdev_counters_get(ftar_dev *d, fdev_counters *out);
 
+/* FTAR_TRACE (test instrumentation; tests/fence_check.py): a per-rank log of every launch with
+ * the registered regions it reads and writes and its system-scope release / acquire, every
+ * fenced marker, drain, gate verdict, and the barrier arrivals the schedules note.  Nothing is
+ * logged (and nothing costs anything) unless fdev_trace_open was called. */
+int fdev_trace_open(ftar_dev *d, const char *path);
+/* name [base, base + bytes) as buffer `name` of original rank `owner` (own or peer mapping) */
+void fdev_trace_region(ftar_dev *d, const void *base, size_t bytes, int owner, const char *name);
+void fdev_trace_unregion(ftar_dev *d, const void *base);
+/* memory this rank's launches did not write but the caller did (an exported send buffer) */
+void fdev_trace_external_write(ftar_dev *d, const void *p, size_t bytes);
+void fdev_trace_note(ftar_dev *d, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+
 /* Standalone local reduce on a caller stream (MPI_Reduce_local). */
 int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream);
 int fdev_set_reduce_variant(int v);

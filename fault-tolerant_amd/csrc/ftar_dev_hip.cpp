@@ -7,10 +7,12 @@
 
 #include <hip/hip_runtime.h>
 
+#include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <string>
 #include <vector>
 
 #include "ftar_dev.h"
@@ -149,6 +151,7 @@ struct ftar_dev {
         unsigned grid, seq;
         ftar::KSegList L;
         ftar::TreeBatch B;
+        std::string tr_rw; // the launch's regions (FTAR_TRACE), for the relaunch's line
     } gp[2];
     int gate_relaunches;
     unsigned tree_unroll;          // FDEV_KNOB_TREE_UNROLL
@@ -162,6 +165,21 @@ struct ftar_dev {
     int big_pending;               // the pending gated launch is a relayed (mid-size) one
     unsigned relay_min;            // FTAR_GATE_RELAY_MIN: short gated launches of this many workgroups or
                                    // more relay their gate too (one PCIe poller instead of one per workgroup)
+    // FTAR_TRACE (test instrumentation, tests/fence_check.py): every launch with the regions it
+    // reads and writes, its release / acquire, every fenced marker, drain, gate verdict and
+    // barrier, one line each.  Off (trace == nullptr) in every measured run.
+    FILE *trace;
+    struct Region {
+        uintptr_t base;
+        size_t bytes;
+        int owner;
+        std::string name;
+    };
+    std::vector<Region> regions;
+    int tr_fenced;     // note_launch recorded a fenced marker in front of the launch being traced
+    int tr_drop;       // FTAR_TRACE_DROP (test-only): 1 = marker drains without their system fence, 2 = no acquires
+    hipEvent_t nofence_main, nofence_bg; // the unfenced markers of tr_drop = 1
+    unsigned long long tr_n;
 };
 
 extern "C" {
@@ -269,6 +287,10 @@ int fdev_open(int device, ftar_dev **out)
     }
     d->h2d = d->d2h = nullptr;
     d->fence_d2h = nullptr;
+    d->trace = nullptr;
+    d->tr_fenced = d->tr_drop = 0;
+    d->nofence_main = d->nofence_bg = nullptr;
+    d->tr_n = 0;
     memset(d->h2d_done, 0, sizeof(d->h2d_done));
     // Peer access to every other GPU of the node: the exchanges read peers' HBM.
     for (int p = 0; p < ndev; p++) {
@@ -308,6 +330,9 @@ void fdev_close(ftar_dev *d)
     if (d->sig_flag) (void)hipHostFree(d->sig_flag);
     if (d->gate_dw) (void)hipFree(d->gate_dw);
     if (d->fence_pre) (void)hipEventDestroy(d->fence_pre);
+    if (d->nofence_main) (void)hipEventDestroy(d->nofence_main);
+    if (d->nofence_bg) (void)hipEventDestroy(d->nofence_bg);
+    if (d->trace) fclose(d->trace);
     delete d;
 }
 
@@ -463,6 +488,87 @@ int fdev_unimport(ftar_dev *d, void *ptr)
     return 0;
 }
 
+// ---- FTAR_TRACE ---------------------------------------------------------------------------
+// A launch's line: `L <n> s=<m|b> sig=<tag> rel=<0|1> acq=<0|1> fence=<0|1> gate=<seq> eng=<k|sdma>
+// r=<regions read> w=<regions written> sw=<staged before the gate> stag=<tag>`, a region as
+// owner:name:offset:bytes (only the registered ones: the workspaces, the exported send buffers and
+// their peer mappings).  `rel` = the kernel releases its stores at system scope before it signals
+// (signal_done), `acq` = it invalidates before its loads (signal_acquire), `fence` = a fenced marker
+// was queued right in front of it.  tests/fence_check.py checks the cross-rank rules on the lines.
+static void tr(ftar_dev *d, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static void tr(ftar_dev *d, const char *fmt, ...)
+{
+    if (!d->trace) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vfprintf(d->trace, fmt, ap);
+    va_end(ap);
+    fputc('\n', d->trace);
+}
+
+struct TrRange {
+    const void *p;
+    size_t n;
+};
+
+static void tr_fmt(const ftar_dev *d, const std::vector<TrRange> &v, std::string &out)
+{
+    char buf[160];
+    for (const TrRange &r : v) {
+        if (!r.p || !r.n) continue;
+        const uintptr_t a = (uintptr_t)r.p;
+        for (const ftar_dev::Region &g : d->regions)
+            if (a >= g.base && a < g.base + g.bytes) {
+                snprintf(buf, sizeof(buf), "%d:%s:%zu:%zu,", g.owner, g.name.c_str(), (size_t)(a - g.base), r.n);
+                out += buf;
+                break;
+            }
+    }
+    if (out.empty()) out = "-";
+}
+
+// The regions of a launch: "r=... w=..." (the relaunch of a gated plan reuses the text)
+static std::string tr_rw(const ftar_dev *d, const std::vector<TrRange> &rd, const std::vector<TrRange> &wr)
+{
+    if (!d->trace) return std::string();
+    std::string a, b;
+    tr_fmt(d, rd, a);
+    tr_fmt(d, wr, b);
+    return "r=" + a + " w=" + b;
+}
+
+static void tr_launch(ftar_dev *d, hipStream_t st, const ftar::KSignal *sig, const std::string &rw, unsigned gate,
+                      const char *eng, const std::string &staged = std::string(), unsigned stag = 0)
+{
+    if (!d->trace) return;
+    const bool rel = sig && sig->cnt;
+    const bool acq = sig && (sig->cnt || sig->gate) && sig->acquire;
+    tr(d, "L %llu s=%c sig=%u rel=%d acq=%d fence=%d gate=%u eng=%s %s sw=%s stag=%u", ++d->tr_n,
+       st == d->stream ? 'm' : 'b', rel ? sig->tag : 0u, rel ? 1 : 0, acq ? 1 : 0, d->tr_fenced, gate, eng, rw.c_str(),
+       staged.empty() ? "-" : staged.c_str(), stag);
+    d->tr_fenced = 0;
+}
+
+static void seg_ranges(const fdev_seg *segs, int nseg, size_t es, std::vector<TrRange> &rd, std::vector<TrRange> &wr)
+{
+    for (int i = 0; i < nseg; i++) {
+        const size_t b = segs[i].n * es;
+        rd.push_back({segs[i].x, b});
+        if (segs[i].kind != FDEV_COPY) rd.push_back({segs[i].y, b});
+        wr.push_back({segs[i].out, b});
+        wr.push_back({segs[i].out2, b});
+    }
+}
+
+static void batch_ranges(const ftar::TreeBatch &B, int nsrc, size_t es, std::vector<TrRange> &rd,
+                         std::vector<TrRange> &wr)
+{
+    for (int t = 0; t < B.nt; t++) {
+        for (int j = 0; j < nsrc; j++) rd.push_back({B.t[t].src[j], B.t[t].n * es});
+        wr.push_back({B.t[t].out, B.t[t].n * es});
+    }
+}
+
 // The background stream exists only in ranks that use it (Raben's step-0 redundancy
 // copy with a spare): every stream is a hardware queue, and ranks that share a GPU (a
 // spare beside its partner, the one-GPU test box) time-slice once the device's queue
@@ -504,8 +610,13 @@ static void note_launch(ftar_dev *d, hipStream_t st, unsigned grid, bool can_sig
     // anything queued behind a closed gate would wait for it: the gated launch is given up
     // (opened as skip; it returns untouched) -- its caller finds the gate no longer pending
     if (d->gate_pending) (void)fdev_gate_open(d, 1);
+    d->tr_fenced = 0;
+    const bool acquire = d->need_acquire && d->tr_drop != 2; // tr_drop 2: TEST-ONLY, acquires left out
     if (st != d->stream) {
-        if (d->need_acquire && d->fence_bg) (void)hipEventRecord(d->fence_bg, st);
+        if (acquire && d->fence_bg) {
+            (void)hipEventRecord(d->fence_bg, st);
+            d->tr_fenced = 1;
+        }
         return;
     }
     if (can_signal && sig && d->flag_sync && grid <= d->flag_max) {
@@ -513,10 +624,13 @@ static void note_launch(ftar_dev *d, hipStream_t st, unsigned grid, bool can_sig
         sig->cnt = d->sig_cnt;
         sig->flag = d->sig_flag;
         sig->tag = ++d->sig_tag;
-        sig->acquire = (unsigned)d->need_acquire;
+        sig->acquire = (unsigned)acquire;
         d->signalled++;
     } else {
-        if (d->need_acquire) (void)hipEventRecord(d->fence_main, st);
+        if (acquire) {
+            (void)hipEventRecord(d->fence_main, st);
+            d->tr_fenced = 1;
+        }
         d->need_acquire = 0;
         d->unsignalled++;
     }
@@ -567,6 +681,11 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
     if (grid == 0) return 0;
     L.nt_store = nt_store();
     note_launch(d, st, grid, true, &L.sig);
+    if (d->trace) {
+        std::vector<TrRange> rd, wr;
+        seg_ranges(segs, nseg, es, rd, wr);
+        tr_launch(d, st, &L.sig, tr_rw(d, rd, wr), 0, "k");
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
         e0 = get_event(d);
@@ -608,6 +727,13 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
         if (e0) (void)hipEventRecord(e0, d->stream);
     }
     note_launch(d, d->stream, ~0u, false, nullptr);
+    if (d->trace) {
+        std::vector<TrRange> rd, wr;
+        for (int j = 0; j < nsrc; j++) rd.push_back({src[j], n * es});
+        wr.push_back({out, n * es});
+        for (int o = 0; o < nmore; o++) wr.push_back({more[o], n * es});
+        tr_launch(d, d->stream, nullptr, tr_rw(d, rd, wr), 0, "k");
+    }
     // pieces of at most max_blocks vector workgroups (plan_tree refuses larger bodies)
     const unsigned u = (nsrc == 4 || nsrc == 8) ? d->tree_unroll : 1u;
     const size_t piece = (size_t)d->max_blocks * 256 * u * (16 / es);
@@ -666,7 +792,7 @@ static ftar::KSignal arm_gate(ftar_dev *d, double link, double hbm)
     k.cnt = d->sig_cnt;
     k.flag = d->sig_flag;
     k.tag = ++d->sig_tag;
-    k.acquire = 1u;
+    k.acquire = d->tr_drop == 2 ? 0u : 1u; // tr_drop 2: TEST-ONLY
     k.gate = gate_word(d, d->gate_seq);
     k.gate_val = 2u * d->gate_seq;
     k.err = gate_err(d, d->gate_seq);
@@ -781,6 +907,18 @@ int fdev_tree_batch_staged_gated(ftar_dev *d, int dtype, int op, const void *con
         d->pre_gate_any = 1;               // the drain before the barrier waits for "staged"
         d->pre_gate_tag = stage_tag;
     }
+    if (d->trace) {
+        std::vector<TrRange> rd, wr, sw;
+        batch_ranges(B, nsrc, es, rd, wr);
+        const std::string rw = tr_rw(d, rd, wr);
+        d->gp[d->gate_seq & 1].tr_rw = rw;
+        std::string st;
+        if (stage_tag) {
+            sw.push_back({stage_dst, stage_n * es});
+            tr_fmt(d, sw, st);
+        }
+        tr_launch(d, d->stream, &B.sig, rw, d->gate_seq, "k", st, stage_tag);
+    }
     hipError_t e = ftar::launch_tree_batch(dtype, op, nsrc, B, grid, d->stream);
     if (e != hipSuccess) return set_err(e, "tree_batch_kernel launch (gated)");
     d->gate_pending = 1;
@@ -799,6 +937,7 @@ int fdev_tree_batch_gated(ftar_dev *d, int dtype, int op, const void *const *src
 int fdev_gate_open(ftar_dev *d, int skip)
 {
     if (!d->gate_pending) return 0;
+    tr(d, "G %u %s", d->gate_seq, skip ? "skip" : "go");
     __atomic_store_n(gate_word(d, d->gate_seq), 2u * d->gate_seq + (skip ? 1u : 0u), __ATOMIC_RELEASE);
     if (!skip) {
         d->ctr.link_bytes += d->gate_link;
@@ -863,6 +1002,11 @@ int fdev_tree_batch(ftar_dev *d, int dtype, int op, const void *const *src, int 
     d->ctr.link_bytes += link;
     d->ctr.hbm_bytes += hbm;
     note_launch(d, d->stream, grid, true, &B.sig);
+    if (d->trace) {
+        std::vector<TrRange> rd, wr;
+        batch_ranges(B, nsrc, esize_of(dtype), rd, wr);
+        tr_launch(d, d->stream, &B.sig, tr_rw(d, rd, wr), 0, "k");
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
         e0 = get_event(d);
@@ -899,6 +1043,7 @@ static int run_gated_relayed(ftar_dev *d, int dtype, int op, const ftar::SegIn *
     if (grid == 0) return 0;
     L.nt_store = nt_store();
     HIPCHK(hipEventRecord(d->fence_pre, d->stream)); // the work before the gate, released and drainable
+    tr(d, "M pre");
     d->need_acquire = 0;
     L.sig = arm_gate(d, link, hbm);
     d->signalled--; // arm_gate counted a signalled launch: this one drains through a marker
@@ -907,6 +1052,19 @@ static int run_gated_relayed(ftar_dev *d, int dtype, int op, const ftar::SegIn *
     L.sig.gate_poll = d->gate_dw + d->gate_seq % ftar::kGateSlots;
     L.sig.gate_dev = d->gate_dw + 32 + d->gate_seq % ftar::kGateSlots;
     keep_plan(d, 0, dtype, op, 0, grid, &L, nullptr);
+    if (d->trace) {
+        std::vector<TrRange> rd, wr;
+        for (int i = 0; i < nseg; i++) {
+            rd.push_back({in[i].x, in[i].n * es});
+            if (in[i].kind != ftar::kCopy) rd.push_back({in[i].y, in[i].n * es});
+            wr.push_back({in[i].out, in[i].n * es});
+            wr.push_back({in[i].out2, in[i].n * es});
+        }
+        const std::string rw = tr_rw(d, rd, wr);
+        d->gp[d->gate_seq & 1].tr_rw = rw;
+        d->tr_fenced = 0;
+        tr_launch(d, d->stream, &L.sig, rw, d->gate_seq, "k");
+    }
     hipError_t e = ftar::launch_segments(dtype, op, L, grid, d->stream);
     if (e != hipSuccess) return set_err(e, "segment_kernel launch (gated, relayed)");
     d->gate_pending = 1;
@@ -959,6 +1117,19 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
         d->pre_gate_any = 1;
         d->pre_gate_tag = stage_tag;
     }
+    if (d->trace) {
+        std::vector<TrRange> rd, wr, sw;
+        seg_ranges(segs, nseg, es, rd, wr);
+        const std::string rw = tr_rw(d, rd, wr);
+        d->gp[d->gate_seq & 1].tr_rw = rw;
+        std::string st;
+        if (stage_tag) {
+            sw.push_back({stage_dst, stage_n * es});
+            tr_fmt(d, sw, st);
+        }
+        d->tr_fenced = 0;
+        tr_launch(d, d->stream, &L.sig, rw, d->gate_seq, "k", st, stage_tag);
+    }
     hipError_t e = ftar::launch_segments(dtype, op, L, grid, d->stream);
     if (e != hipSuccess) return set_err(e, "segment_kernel launch (gated)");
     d->gate_pending = 1;
@@ -1000,6 +1171,7 @@ int fdev_copy(ftar_dev *d, int bg, void *dst, const void *src, size_t bytes, int
         d->ctr.hbm_bytes += 2.0 * (double)bytes;
     }
     note_launch(d, st, ~0u, false, nullptr);
+    if (d->trace) tr_launch(d, st, nullptr, tr_rw(d, {{src, bytes}}, {{dst, bytes}}), 0, "sdma");
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
         e0 = get_event(d);
@@ -1050,6 +1222,11 @@ static int harvest(ftar_dev *d);
 static int sync_stream(ftar_dev *d, hipStream_t st, int (*poll)(void *), void *arg)
 {
     hipEvent_t fence = st == d->bg ? d->fence_bg : d->fence_main;
+    if (d->tr_drop == 1) { // TEST-ONLY (FTAR_TRACE_DROP=release): the drain without its system fence
+        hipEvent_t &nf = st == d->bg ? d->nofence_bg : d->nofence_main;
+        if (!nf) HIPCHK(hipEventCreateWithFlags(&nf, hipEventDisableTiming | hipEventDisableSystemFence));
+        fence = nf;
+    }
     HIPCHK(hipEventRecord(fence, st));
     for (;;) {
         hipError_t e = hipEventQuery(fence);
@@ -1060,6 +1237,7 @@ static int sync_stream(ftar_dev *d, hipStream_t st, int (*poll)(void *), void *a
             if (r) return r;
         }
     }
+    tr(d, "D %s %c", d->tr_drop == 1 ? "nf" : "mk", st == d->bg ? 'b' : 'm');
     return 0;
 }
 
@@ -1107,6 +1285,8 @@ static int verify_gate(ftar_dev *d, int (*poll)(void *), void *arg)
         fprintf(stderr, "ftar: device %d: gated launch %u %s: relaunched\n", d->device, g.seq,
                 redo++ ? "ran after a relaunched one" : "was given up by the device (gate timeout)");
         HIPCHK(hipEventRecord(d->fence_main, d->stream));
+        d->tr_fenced = 1;
+        tr_launch(d, d->stream, nullptr, g.tr_rw, 0, "k");
         hipError_t e = g.batch ? ftar::launch_tree_batch(g.dtype, g.op, g.nsrc, g.B, g.grid, d->stream)
                                : ftar::launch_segments(g.dtype, g.op, g.L, g.grid, d->stream);
         if (e != hipSuccess) return set_err(e, "relaunch of a timed-out gated launch");
@@ -1133,6 +1313,7 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
         d->signalled = d->force_fence = 0;
         d->unsignalled = 1; // the gated launch, drained through a marker after its gate opens
         if (rc) return rc;
+        tr(d, "D pre");
         rc = verify_gate(d, poll, arg);
         if (rc) return rc;
         return harvest(d);
@@ -1142,6 +1323,7 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
         // signalled, the gated launch checked; nothing is queued behind it, see note_launch),
         // never a marker behind the gate
         rc = d->pre_gate_any ? wait_signal(d, d->pre_gate_tag, poll, arg) : 0;
+        if (!rc && d->pre_gate_any) tr(d, "D sig %u", d->pre_gate_tag);
         d->need_acquire = 1;
         d->pre_gate_any = 0;
         d->unsignalled = d->force_fence = 0;
@@ -1159,6 +1341,7 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
         // only signalled launches: each workgroup released its stores at system scope before
         // the last one raised the flag, so the data is visible to the peers and the host
         rc = wait_signal(d, d->sig_tag, poll, arg);
+        if (!rc) tr(d, "D sig %u", d->sig_tag);
         d->need_acquire = 1;
     } else {
         rc = sync_stream(d, d->stream, poll, arg);
@@ -1282,6 +1465,7 @@ int fdev_sync_d2h(ftar_dev *d, int (*poll)(void *), void *arg)
 int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t bytes)
 {
     note_launch(d, d->stream, ~0u, false, nullptr);
+    if (d->trace) tr_launch(d, d->stream, nullptr, tr_rw(d, {}, {{dst, bytes}}), 0, "h2d");
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d->stream));
     return fdev_sync(d, nullptr, nullptr);
 }
@@ -1289,6 +1473,7 @@ int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t bytes)
 int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t bytes)
 {
     note_launch(d, d->stream, ~0u, false, nullptr);
+    if (d->trace) tr_launch(d, d->stream, nullptr, tr_rw(d, {{src, bytes}}, {}), 0, "d2h");
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, d->stream));
     return fdev_sync(d, nullptr, nullptr);
 }
@@ -1322,6 +1507,67 @@ static int check_local_ptr(const void *ptr, size_t bytes, int dev)
     if (a.type == hipMemoryTypeHost) return !host_same_va(a) || !range_inside(ptr, bytes);
     if (a.type != hipMemoryTypeDevice || a.device != dev) return 1;
     return !range_inside(ptr, bytes);
+}
+
+int fdev_trace_open(ftar_dev *d, const char *path)
+{
+    if (d->trace) return 0;
+    d->trace = fopen(path, "w");
+    if (!d->trace) {
+        snprintf(g_err, sizeof(g_err), "FTAR_TRACE: cannot open %s", path);
+        return 13;
+    }
+    setvbuf(d->trace, nullptr, _IOLBF, 0); // a killed rank leaves every line it wrote
+    const char *dr = getenv("FTAR_TRACE_DROP");
+    d->tr_drop = !dr ? 0 : !strcmp(dr, "release") ? 1 : !strcmp(dr, "acquire") ? 2 : 0;
+    tr(d, "# ftar trace: device %d, flag_sync %d, drop %d", d->device, d->flag_sync, d->tr_drop);
+    return 0;
+}
+
+void fdev_trace_region(ftar_dev *d, const void *base, size_t bytes, int owner, const char *name)
+{
+    if (!d->trace || !base) return;
+    for (ftar_dev::Region &g : d->regions)
+        if (g.base == (uintptr_t)base) {
+            g.bytes = bytes;
+            g.owner = owner;
+            g.name = name;
+            tr(d, "R %d %s %zu", owner, name, bytes);
+            return;
+        }
+    d->regions.push_back(ftar_dev::Region{(uintptr_t)base, bytes, owner, name});
+    tr(d, "R %d %s %zu", owner, name, bytes);
+}
+
+void fdev_trace_unregion(ftar_dev *d, const void *base)
+{
+    if (!d->trace || !base) return;
+    for (size_t i = 0; i < d->regions.size(); i++)
+        if (d->regions[i].base == (uintptr_t)base) {
+            tr(d, "U %d %s", d->regions[i].owner, d->regions[i].name.c_str());
+            d->regions.erase(d->regions.begin() + (long)i);
+            return;
+        }
+}
+
+// A write this rank's own launches did not make (the caller's send buffer, exported to the
+// peers as it is): `X owner:name:offset:bytes`
+void fdev_trace_external_write(ftar_dev *d, const void *p, size_t bytes)
+{
+    if (!d->trace) return;
+    std::string w;
+    tr_fmt(d, {{p, bytes}}, w);
+    tr(d, "X %s", w.c_str());
+}
+
+void fdev_trace_note(ftar_dev *d, const char *fmt, ...)
+{
+    if (!d->trace) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vfprintf(d->trace, fmt, ap);
+    va_end(ap);
+    fputc('\n', d->trace);
 }
 
 int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, void *stream)

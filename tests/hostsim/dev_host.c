@@ -506,3 +506,10 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
 }
 
 int fdev_export_retries(const ftar_dev *d) { return 0; }
+
+/* FTAR_TRACE is GPU instrumentation (cache release / acquire): nothing to log here */
+int fdev_trace_open(ftar_dev *d, const char *path) { return 0; }
+void fdev_trace_region(ftar_dev *d, const void *base, size_t bytes, int owner, const char *name) {}
+void fdev_trace_unregion(ftar_dev *d, const void *base) {}
+void fdev_trace_external_write(ftar_dev *d, const void *p, size_t bytes) {}
+void fdev_trace_note(ftar_dev *d, const char *fmt, ...) {}

@@ -1,0 +1,111 @@
+"""Cross-device fence discipline on the GPU.
+
+Every rank of a device-resident job (bin/ftbench under ftrun, all ranks on GPU 0) logs its
+launches, drains, fenced markers, gate verdicts and barriers (FTAR_TRACE), and
+tests/fence_check.py checks the two rules the node's cross-GPU visibility rests on over
+all ranks' logs: every peer read after barrier k sees only writes their owner released at
+system scope before arriving at k, and the reading launch invalidates (acquire) or follows
+a fenced marker with no stale read of that range in between.  On one GPU a violation cannot
+give a wrong result (one HBM behind the same L2s), so the discipline is checked directly,
+for every transport form and across the small-call thresholds.  A deliberately removed
+release (FTAR_TRACE_DROP=release: the marker drains without their system fence) and a
+removed acquire (FTAR_TRACE_DROP=acquire) must each fail it.
+
+FTAR_GPU_FENCE_WIDE=1 adds the 8-rank and remaining size/form combinations."""
+import json
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+import fence_check as FC
+import harness as H
+
+pytestmark = pytest.mark.gpu
+
+MIB = 1 << 20
+# (ranks, algo, float32 elements, options): every form and the sizes on both sides of the
+# small-call thresholds (1 MiB: staging, one-shot, gates, completion flags)
+BASE = [
+    (2, "raben", 1, {}),                                   # 4 B: one-shot, staged, gated
+    (4, "raben", 16384, {}),                               # 64 KiB one-shot
+    (4, "raben", 262140, {}),                              # 1 MiB - 16 B
+    (4, "raben", 262148, {}),                              # 1 MiB + 16 B: two-launch mesh, read in place
+    (4, "raben", MIB, {}),                                 # 4 MiB mesh
+    (4, "raben", MIB, {"FTAR_TREE_UNROLL": "2"}),          # mesh_u2
+    (4, "raben", MIB, {"FTAR_PUSH": "1"}),                 # mesh_push
+    (4, "raben", MIB, {"FTAR_PUSH": "2"}),                 # mesh_push2
+    (4, "raben", 16384, {"FTAR_PUSH": "2", "FTAR_ONESHOT_MAX": "0"}),
+    (4, "raben", MIB, {"FTAR_GATE_MAX": str(16 * MIB)}),   # mid-size gate: allgather behind the tree
+    (4, "raben", MIB, {"FTAR_MESH": "0", "FTAR_RELAY": "1", "FTAR_RELAY_MIN": "0"}),  # relay2hop
+    (4, "raben", MIB, {"FTAR_MESH": "0", "FTAR_RELAY": "0"}),                         # direct
+    (4, "raben", MIB, {"FTAR_MESH": "0", "FTAR_COPY_ENGINE": "1"}),                   # copy engine
+    (5, "raben", MIB, {}),                                 # spare: pre-step, step by step, post-step
+    (3, "raben", 16384, {}),
+    (4, "rd", 1, {}),
+    (4, "rd", 16384, {}),                                  # gated steps, staged
+    (4, "rd", 262148, {}),
+    (4, "rd", MIB, {"FTAR_GATE_MAX": str(16 * MIB)}),      # mid-size gated steps 1..
+    (4, "rd", MIB, {"FTAR_RELAY_MIN": "0"}),               # relayed steps
+    (5, "rd", 16384, {}),                                  # pre-step + fan-out
+    (4, "raben", 16384, {"FTAR_FLAG_SYNC": "0"}),          # fenced-marker drains only
+    (4, "raben", 64 * MIB, {}),                            # 256 MiB mesh
+    (4, "raben", 64 * MIB, {"FTAR_GATE_MAX": str(256 * MIB)}),  # mesh_gated_ag at the headline size
+]
+WIDE = [
+    (8, "raben", 1, {}), (8, "raben", 16384, {}), (8, "raben", 262140, {}), (8, "raben", 262148, {}),
+    (8, "raben", MIB, {"FTAR_TREE_UNROLL": "4"}), (8, "raben", MIB, {"FTAR_PUSH": "2"}),
+    (8, "raben", MIB, {"FTAR_MESH": "0", "FTAR_RELAY_MIN": "0"}), (8, "rd", MIB, {"FTAR_RELAY_MIN": "0"}),
+    (8, "rd", 16384, {}), (2, "rd", 262148, {}), (2, "raben", 64 * MIB, {}), (8, "raben", 64 * MIB, {}),
+]
+CASES = BASE + (WIDE if os.environ.get("FTAR_GPU_FENCE_WIDE") == "1" else [])
+
+
+def _trace_job(p, algo, n, opts, drop=None, calls=3):
+    tmp = tempfile.mkdtemp(prefix="ftar_fence_")
+    env = dict(os.environ, FTBENCH_PATTERN="1", FTAR_TRACE=os.path.join(tmp, "t"), **opts)
+    env.pop("FTAR_KILL", None)
+    env.pop("FTAR_TRACE_DROP", None)
+    if drop:
+        env["FTAR_TRACE_DROP"] = drop
+    cp = subprocess.run([os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ",".join("0" * p),
+                         os.path.join(H.PKG, "bin", "ftbench"), algo, str(n), str(calls)], env=env,
+                        capture_output=True, text=True, timeout=240)
+    assert cp.returncode == 0, cp.stderr[-2000:]
+    lines = [json.loads(ln) for ln in cp.stdout.splitlines() if ln.startswith("{")]
+    assert sorted(ln["rank"] for ln in lines) == list(range(p)), cp.stdout[-1000:]
+    for ln in lines:
+        assert all(c["rc"] == 0 and c["uniform"] for c in ln["calls"]), ln
+    logs = FC.load(os.path.join(tmp, "t"))
+    assert sorted(logs) == list(range(p))
+    return FC.check(logs), logs
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("p,algo,n,opts", CASES, ids=[f"{a}-p{p}-{4 * n}B-" + ("_".join(f"{k[5:]}{v}" for k, v in o.items())
+                                                                                 or "default")
+                                                      for p, a, n, o in CASES])
+def test_fence_discipline(p, algo, n, opts):
+    rep, logs = _trace_job(p, algo, n, opts)
+    assert rep.ok, (rep.release[:5], rep.acquire[:5])
+    assert rep.reads_checked > 0  # peer reads were seen and checked
+    assert all(lg.arrive and lg.passed for lg in logs.values())
+
+
+@pytest.mark.timeout(300)
+def test_dropped_release_fails_the_check():
+    """The mesh's tree is drained by a fenced marker before the reduce-scatter's barrier; with
+    that marker's system fence removed (test-only switch) the allgather's peer reads of the
+    blocks it wrote are unreleased reads, and the checker says so."""
+    rep, _ = _trace_job(4, "raben", MIB, {}, drop="release")
+    assert rep.release, "a removed release went unnoticed"
+
+
+@pytest.mark.timeout(300)
+def test_dropped_acquire_fails_the_check():
+    """Small RD calls drain by completion flags only; each gated step invalidates its caches
+    before reading the peers' accumulators.  With the acquires removed the next call's reads
+    of lines the previous call cached are stale reads, and the checker says so."""
+    rep, _ = _trace_job(4, "rd", 16384, {}, drop="acquire")
+    assert rep.acquire, "a removed acquire went unnoticed"

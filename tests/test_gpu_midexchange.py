@@ -115,14 +115,14 @@ def test_full_size_c3_rd_p8(oracle):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("shape", ["mesh", "push", "push2", "reference"])
+@pytest.mark.parametrize("shape", ["mesh", "reference"] + H.wide("push", "push2"))
 def test_full_size_c4_raben_p8(oracle, shape):
     """configs[3]: Rabenseifner, 256 MiB float32 SUM, 8 ranks -- the default one-hop
     mesh, its push form, and the reference's shape (step by step, pairwise, step-0 full
     exchange)."""
     # one device-resident 256 MiB call per rank (no host-pipeline chunking)
-    env = dict(REFERENCE_SHAPE if shape == "reference" else {"FTAR_PUSH": "1"} if shape == "push" else
-               {"FTAR_PUSH": "2"} if shape == "push2" else {}, FTAR_HOST_PIPE="0")
+    env = dict(REFERENCE_SHAPE if shape == "reference" else dict(H.MESH_FORM, FTAR_PUSH={"push": "1", "push2": "2"}
+                                                                  .get(shape, "0")), FTAR_HOST_PIPE="0")
     o, r = _check(oracle.rabenseifner, "raben", oracle.random_inputs(8, FULL, seed=704), env=env, timeout=600)
     mesh_steps = {st[0][9] for st in r.status.values()}
     assert mesh_steps == ({0} if shape == "reference" else {2}), r.status
@@ -168,7 +168,7 @@ KILL_COUNTS = [int(c) for c in os.environ.get("FTAR_GPU_KILL_COUNTS", "").split(
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("seed,count", [(s, c) for s in _seeds("FTAR_GPU_KILL_SEEDS", [0, 1])
+@pytest.mark.parametrize("seed,count", [(s, c) for s in _seeds("FTAR_GPU_KILL_SEEDS", [0] + H.wide(1))
                                         for c in (KILL_COUNTS or [(1 << 20) + 3])] +
                          ([] if KILL_COUNTS else [(0, 1031)]))
 def test_random_kill_points_gpu(oracle, seed, count):

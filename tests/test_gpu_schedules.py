@@ -174,7 +174,7 @@ def test_driver_golden_checksums_max_size(algo, p):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("algo,p", [("raben", 2), ("rd", 2), ("raben", 3)])
+@pytest.mark.parametrize("algo,p", [("rd", 2), ("raben", 3)] + H.wide(("raben", 2)))
 def test_beyond_2g_elements(algo, p):
     """2^31 + 7 float32 elements per rank (8 GiB vectors, ~50 GiB of HBM per rank with the
     workspace): the C ABI takes size_t counts (the reference's int count stops at 2^31-1).
@@ -197,7 +197,7 @@ def test_beyond_2g_elements(algo, p):
         assert c["rc"] == 0 and c["comm_size"] == p and c["uniform"], ln
 
 
-RELAY_ALL = {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}  # the step-by-step schedule, relayed
+RELAY_ALL = {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0", "FTAR_RELAY": "1"}  # the step-by-step schedule, relayed
 
 
 @pytest.mark.parametrize("algo", ["raben", "rd"])
@@ -276,9 +276,18 @@ def test_torch_device_buffers(oracle, algo, p, mode):
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
 
 
-@pytest.mark.parametrize("push,unroll", [("0", "1"), ("1", "1"), ("2", "1"), ("0", "2"), ("0", "4"), ("1", "4")])
-@pytest.mark.parametrize("p,op,count", [(2, 0, 100003), (4, 0, 100003), (8, 0, 65536 + 5), (4, 2, 4099), (8, 3, 4099),
-                                        (4, 0, (1 << 22) + 13), (8, 1, (1 << 20) + 3)])
+MESH_SHAPES = [(2, 0, 100003), (4, 0, 100003), (8, 0, 65536 + 5), (4, 2, 4099), (8, 3, 4099), (4, 0, (1 << 22) + 13),
+               (8, 1, (1 << 20) + 3)]
+MESH_FORMS = [("0", "1"), ("1", "1"), ("2", "1"), ("0", "2"), ("0", "4"), ("1", "4")]
+# every shape in the pull form, each other form on two shapes (a ragged / NaN-order one and a
+# multi-workgroup one); the whole matrix under FTAR_GPU_WIDE=1
+MESH_CASES = [s + f for f in MESH_FORMS for s in MESH_SHAPES] if H.WIDE else \
+    [s + ("0", "1") for s in MESH_SHAPES] + \
+    [s + f for f in MESH_FORMS[1:3] for s in (MESH_SHAPES[2], MESH_SHAPES[3])] + \
+    [s + f for f in MESH_FORMS[3:] for s in (MESH_SHAPES[4], MESH_SHAPES[5])]
+
+
+@pytest.mark.parametrize("p,op,count,push,unroll", MESH_CASES)
 def test_mesh_schedule(oracle, p, op, count, push, unroll):
     """Power of two without a spare: one-hop reduce-scatter -- a tree kernel over p - 1
     peer pulls, or (FTAR_PUSH=1) p - 1 remote-store copies into the owners followed by the
@@ -293,7 +302,8 @@ def test_mesh_schedule(oracle, p, op, count, push, unroll):
         ins = H.with_specials(ins, p + op)
     # one device-resident call (the host pipeline would split >= 16 MiB into chunk calls)
     o, r = _check(oracle.rabenseifner, "raben", ins, op=op,
-                  env={"FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0", "FTAR_PUSH": push, "FTAR_TREE_UNROLL": unroll})
+                  env=dict(H.MESH_FORM, FTAR_ONESHOT_MAX="0", FTAR_HOST_PIPE="0", FTAR_PUSH=push,
+                           FTAR_TREE_UNROLL=unroll))
     assert all(st[0][9] == 2 for st in r.status.values()), r.status
 
 
@@ -307,7 +317,7 @@ def test_oneshot_schedule(oracle, p, op, count):
     ins = oracle.random_inputs(p, count, seed=p * 11 + op, dtype=dt)
     if op >= 2:
         ins = H.with_specials(ins, p + op)
-    o, r = _check(oracle.rabenseifner, "raben", ins, op=op, iters=2, env={"FTAR_ONESHOT_MAX": str(1 << 20)})
+    o, r = _check(oracle.rabenseifner, "raben", ins, op=op, iters=2, env=dict(H.MESH_FORM, FTAR_ONESHOT_MAX=str(1 << 20)))
     u = np.uint32
     for w, st in r.status.items():
         assert st[0][9] == 1 and st[1][9] == 1, (w, st)
