@@ -75,10 +75,10 @@ def test_rd_single_kill(oracle, kill):
     _check(oracle.recursive_doubling, "rd", oracle.random_inputs(p, 65536 + 3, seed=4), [kill])
 
 
-RECOVERING_P5 = [("raben", k) for k in [(0, 1, 1, 0), (3, 1, 1, 0), (4, 1, 1, 1), (2, 1, 1, 1), (0, 2, 0, 0),
-                                         (4, 2, 0, 1), (3, 1, 1, 3), (2, 2, 0, 3)]] + \
-                [("rd", k) for k in [(0, 1, 1, 0), (3, 1, 1, 0), (4, 1, 1, 1), (2, 1, 1, 1), (1, 1, 1, 3),
-                                     (4, 1, 0, 3), (0, 1, 1, 2), (3, 1, 1, 3)]]
+RECOVERING_P5 = [("raben", k) for k in [(0, 1, 1, 0), (4, 1, 1, 1), (0, 2, 0, 0), (4, 2, 0, 1), (3, 1, 1, 3),
+                                         (2, 2, 0, 3)] + H.wide((3, 1, 1, 0), (2, 1, 1, 1))] + \
+                [("rd", k) for k in [(0, 1, 1, 0), (4, 1, 1, 1), (1, 1, 1, 3), (0, 1, 1, 2)] +
+                 H.wide((3, 1, 1, 0), (2, 1, 1, 1), (4, 1, 0, 3), (3, 1, 1, 3))]
 
 
 @pytest.mark.parametrize("algo,kill", RECOVERING_P5)
@@ -142,7 +142,7 @@ def _golden_checksums():
 
 
 @pytest.mark.parametrize("algo", ["raben", "rd"])
-@pytest.mark.parametrize("p", [4, 6, 8])
+@pytest.mark.parametrize("p", [4, 8] + H.wide(6))
 def test_driver_golden_checksums(algo, p):
     """The drop-in drivers on the GPU against the reference's own recorded results
     (data/data_compare rows committed in tests/golden/ref_checksums.csv): every rank's
@@ -256,9 +256,9 @@ def test_raben_redundancy_always(oracle, p, kill):
            [kill] if kill else [], env={"FTAR_REDUNDANCY": "1"})
 
 
-@pytest.mark.parametrize("algo,p,mode", [("raben", 4, "plain"), ("raben", 4, "inplace"), ("raben", 2, "offset1"),
-                                         ("raben", 8, "inplace_offset3"), ("raben", 3, "inplace"),
-                                         ("rd", 4, "inplace"), ("rd", 4, "offset1")])
+@pytest.mark.parametrize("algo,p,mode", [("raben", 4, "plain"), ("raben", 8, "inplace_offset3"), ("raben", 3, "inplace"),
+                                         ("rd", 4, "offset1")] +
+                         H.wide(("raben", 4, "inplace"), ("raben", 2, "offset1"), ("rd", 4, "inplace")))
 def test_torch_device_buffers(oracle, algo, p, mode):
     """The device-pointer entry points on torch tensors (bench.py's path), bound through
     the Python package: in place, at element offsets, two calls; sbuf untouched."""
@@ -324,10 +324,10 @@ def test_oneshot_schedule(oracle, p, op, count):
         assert np.array_equal(r.outputs[w][1].view(u), o.outputs[w].view(u)), w
 
 
-@pytest.mark.parametrize("p,count,mode", [(4, 4099, {}), (8, 65536 + 5, {"FTAR_PROBE_INPLACE": "1"}),
-                                          (8, 7, {"FTAR_PROBE_OFFSET": "3"}),
+@pytest.mark.parametrize("p,count,mode", [(8, 65536 + 5, {"FTAR_PROBE_INPLACE": "1"}),
                                           (8, (1 << 18) - 1, {"FTAR_PROBE_OFFSET": "1", "FTAR_PROBE_INPLACE": "1"}),
-                                          (4, 1000, {"FTAR_PROBE_REALLOC": "1"})])
+                                          (4, 1000, {"FTAR_PROBE_REALLOC": "1"})] +
+                         H.wide((4, 4099, {}), (8, 7, {"FTAR_PROBE_OFFSET": "3"})))
 def test_oneshot_device_buffers(oracle, p, count, mode):
     """The one-shot mesh on torch device buffers: peers read sbuf in place (staged when
     sbuf == rbuf), misaligned offsets, a re-allocated sbuf; sbuf never written."""
@@ -343,8 +343,12 @@ def test_oneshot_device_buffers(oracle, p, count, mode):
         assert np.array_equal(r.outputs[w][1].view(np.uint32), (sign * o.outputs[w]).view(np.uint32))
 
 
-@pytest.mark.parametrize("form", ["0", str(1 << 20), "push", "push2"])
-@pytest.mark.parametrize("kill", [(3, 1, 1, 2), (0, 2, 0, 1), (5, 1, 0, 0), (2, 1, 1, 3)])
+MESH_KILLS = [(3, 1, 1, 2), (0, 2, 0, 1), (5, 1, 0, 0), (2, 1, 1, 3)]
+
+
+# every kill in both pull forms, the push forms at two of them (all under FTAR_GPU_WIDE=1)
+@pytest.mark.parametrize("kill,form", [(k, f) for f in ("0", str(1 << 20)) for k in MESH_KILLS] +
+                         [(k, f) for f in ("push", "push2") for k in (MESH_KILLS if H.WIDE else MESH_KILLS[2:])])
 def test_mesh_kill_aborts(oracle, kill, form):
     """Any death in the mesh phases (two-launch, one-shot, push) ends the job like the
     reference at p = 8 (no idle rank); (2, 1, 1, 3) dies mid-exchange with its peers'
@@ -433,9 +437,9 @@ def test_device_entry_refuses_pageable_host_memory(algo):
 
 
 @pytest.mark.parametrize("algo,p,env", [
-    ("raben", 4, {}), ("raben", 8, {"FTAR_ONESHOT_MAX": "0"}), ("raben", 2, {}),
-    ("raben", 9, {"FTAR_RELAY_MIN": "0"}), ("rd", 6, {"FTAR_RELAY_MIN": "0"}), ("rd", 8, {}),
-    ("raben", 9, {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"})])
+    ("raben", 8, {"FTAR_ONESHOT_MAX": "0"}), ("raben", 9, {"FTAR_RELAY_MIN": "0"}), ("rd", 6, {"FTAR_RELAY_MIN": "0"}),
+    ("rd", 8, {}), ("raben", 9, {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"})] +
+    H.wide(("raben", 4, {}), ("raben", 2, {})))
 def test_capped_grids_plain_stores(oracle, algo, p, env):
     """One workgroup per CU (FTAR_BLOCKS_PER_CU=1: 256-workgroup grids) so every kernel
     strides over its pieces and the tree launches split, with plain instead of
@@ -484,10 +488,10 @@ def test_kill_logical_bitwise(oracle, algo, p, kill, op):
     assert not o.aborted and o.recoveries >= 1
 
 
-@pytest.mark.parametrize("algo,p,mode", [("raben", 2, {}), ("raben", 4, {}), ("raben", 4, {"FTAR_ONESHOT_MAX": "0"}),
-                                         ("raben", 8, {"FTAR_PROBE_INPLACE": "1", "FTAR_ONESHOT_MAX": "0"}),
+@pytest.mark.parametrize("algo,p,mode", [("raben", 2, {}), ("raben", 8, {"FTAR_PROBE_INPLACE": "1", "FTAR_ONESHOT_MAX": "0"}),
                                          ("raben", 5, {}), ("raben", 4, {"FTAR_MESH": "0", "FTAR_PROBE_OFFSET": "1"}),
-                                         ("rd", 4, {}), ("rd", 6, {"FTAR_PROBE_INPLACE": "1"})])
+                                         ("rd", 6, {"FTAR_PROBE_INPLACE": "1"})] +
+                         H.wide(("raben", 4, {}), ("raben", 4, {"FTAR_ONESHOT_MAX": "0"}), ("rd", 4, {})))
 def test_pinned_host_buffers(oracle, algo, p, mode):
     """The device entry points on pinned host buffers: this rank's kernels read sbuf and
     write rbuf in place over PCIe (zero copy), peers read the staged copy in HBM (host
