@@ -206,7 +206,7 @@ def test_random_two_kills_gpu(oracle, seed):
     import random
     rng = random.Random(1000 + seed)
     n = 0
-    while n < 6:
+    while n < (6 if H.WIDE else 3):
         algo = rng.choice(["raben", "rd"])
         p = rng.choice([9, 11] if algo == "raben" else [6, 8])
         pts = [(v, ph, st, pt) for v in range(p) for ph in ((1, 2) if algo == "raben" else (1,))
@@ -230,7 +230,7 @@ GPU_TRANSPORTS = [{}, {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}, {"FTAR_COPY_ENG
 
 
 @pytest.mark.timeout(900)
-@settings(max_examples=int(os.environ.get("FTAR_GPU_PROPERTY_EXAMPLES", "20")), deadline=None,
+@settings(max_examples=int(os.environ.get("FTAR_GPU_PROPERTY_EXAMPLES", "20" if H.WIDE else "10")), deadline=None,
           suppress_health_check=[HealthCheck.function_scoped_fixture], database=None)
 @given(algo=st.sampled_from(["raben", "rd"]), p=st.integers(2, 8), count=st.integers(1, 300000),
        op=st.integers(0, 3), transport=st.integers(0, len(GPU_TRANSPORTS) - 1), iters=st.integers(1, 2),

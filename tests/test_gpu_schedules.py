@@ -174,7 +174,7 @@ def test_driver_golden_checksums_max_size(algo, p):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("algo,p", [("rd", 2), ("raben", 3)] + H.wide(("raben", 2)))
+@pytest.mark.parametrize("algo,p", [("raben", 3)] + H.wide(("rd", 2), ("raben", 2)))
 def test_beyond_2g_elements(algo, p):
     """2^31 + 7 float32 elements per rank (8 GiB vectors, ~50 GiB of HBM per rank with the
     workspace): the C ABI takes size_t counts (the reference's int count stops at 2^31-1).
