@@ -202,7 +202,6 @@ typedef struct {
     int dst_buf, x_buf;
     int64_t off, n;
     int to_uout; /* also store the result in the caller's output buffer (same offset) */
-    int save_pre; /* REDUCE: the same launch stores the local operand's pre-image into T (same offset) */
 } ftar_pull;
 
 #define FTAR_MAX_PULLS 2

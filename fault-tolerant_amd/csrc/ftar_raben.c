@@ -7,11 +7,14 @@
  * over xGMI (IPC peer mapping) and reduces it into the local window:
  *
  *   RS step 0 (:206-211 full exchange + :231-237 reduce):
- *       W[rw0] = IN[rw0] + peer.IN[rw0]        (reduce half)
- *       T[sw0] = peer.IN[sw0]                  (redundancy copy, FTAR_REDUNDANCY=1 only:
+ *       A0[rw0] = IN[rw0] + peer.IN[rw0]       (reduce half)
+ *       T[sw0] = peer.IN[sw0]                  (redundancy copy, where a spare can use it:
  *                                               a replay otherwise reads peer.IN itself)
- *   RS step k>=1 (:219-237):  W[rwk] = W[rwk] + peer.W[rwk]
+ *   RS step k>=1 (:219-237):  Ak[rwk] = A(k-1)[rwk] + peer.A(k-1)[rwk]
  *   AG step k (:299-315):     W[swk] = peer.W[swk]
+ * The accumulators Ak are W, except with an idle spare, where the steps alternate W and T's
+ * free half (rb_acc) so that no step overwrites its own input: a partner that dies
+ * mid-exchange costs no pre-image (see the reduce-scatter loop).
  *
  * Buffers (exported workspace, ftar_internal.h): IN = this rank's vector after the
  * pre-step (the reference's sbuf after :128), W = rbuf, T = tmp_buf.  The reference's
@@ -45,6 +48,7 @@ typedef struct {
     int steps, adjsize, rem;
     int rank, vrank, corr, has_recov;
     int keep_recov; /* step 0 also pulls the partner's other half into T (recovery data) */
+    int alt;        /* RS accumulators alternate W / T (an idle spare at the call's start; rb_acc) */
     int bg_pending; /* step-0 redundancy copy still running on the background stream */
     int fast_io;    /* power of two, no recovery data: sbuf/rbuf used in place (see below) */
     int out_done;   /* the last allgather step already stored this rank's result in rbuf */
@@ -103,6 +107,19 @@ static void rb_windows(int v, size_t count, int steps, int64_t *rindex, int64_t 
 
 static void *at(const rb_ctx *x, void *base, int64_t idx) { return (char *)base + (size_t)idx * x->es; }
 
+/* The buffer holding every rank's reduce-scatter window after step s (uniform: the same on
+ * every rank and for the whole call).  Without a spare, W: every failure aborts, and the
+ * steps reduce in place.  With a spare a partner's death mid-exchange is recoverable and the
+ * received window must then be discarded (corr, :238-241): the steps reduce OUT OF PLACE,
+ * alternating W and T -- whose half rw0 is free, T holding the partner's other half sw0 -- so
+ * the step's input window stays intact and nothing has to be restored (round 4 stored the
+ * pre-image, rcount x es bytes per step: 96 MiB per 256 MiB call at p = 9).  The parity ends
+ * in W at the last step, where the allgather reads the final blocks.  Every later window lies
+ * in the earlier ones, and a rank only writes its own receive windows, so a partner's send
+ * window at step s stays what it held after step s - 1 (the replay of rb_handler_rs reads it
+ * there). */
+static int rb_acc(const rb_ctx *x, int s) { return (!x->alt || (x->steps - 1 - s) % 2 == 0) ? WS_W : WS_T; }
+
 static int rb_vrank_of(const rb_ctx *x, int cr)
 {
     if (cr < 2 * x->rem) return (cr % 2 == 0) ? cr / 2 : -1;
@@ -127,17 +144,15 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
         if (ag) { /* the last allgather step lands in rbuf: only there (fast_io) or also in W */
             int last = step == 0;
             pl[0] = (ftar_pull){FDEV_COPY, 0, src, WS_W, (x->fast_io && last) ? WS_UOUT : WS_W, WS_W, si[step],
-                                sc[step], !x->fast_io && last, 0};
+                                sc[step], !x->fast_io && last};
             P->npull[cr] = 1;
         } else if (step == 0) { /* fast_io: the local operand is sbuf itself */
-            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, WS_W, x->fast_io ? WS_UIN : WS_IN, ri[0], rc[0], 0, 0};
-            pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0], 0, 0};
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_IN, rb_acc(x, 0), x->fast_io ? WS_UIN : WS_IN, ri[0], rc[0], 0};
+            pl[1] = (ftar_pull){FDEV_COPY, 0, src, WS_IN, WS_T, WS_T, si[0], sc[0], 0};
             P->npull[cr] = x->keep_recov ? 2 : 1;
-        } else {
-            /* with an idle rank a partner's death mid-exchange is recoverable and the pulled
-             * window must then be discarded (corr, :238-241): the pull keeps its pre-image in
-             * T (see the reduce-scatter loop) */
-            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, WS_W, WS_W, WS_W, ri[step], rc[step], 0, x->rem > 0};
+        } else { /* the partner's window of the previous step, reduced into this step's accumulator */
+            pl[0] = (ftar_pull){FDEV_REDUCE, 0, src, rb_acc(x, step - 1), rb_acc(x, step), rb_acc(x, step - 1), ri[step],
+                                rc[step], 0};
             P->npull[cr] = 1;
         }
     }
@@ -204,9 +219,9 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
             }
             run_reduce(x, at(x, W, dri[0]), at(x, IN, dri[0]), at(x, (void *)D0, dri[0]), drc[0],
                        x->keep_recov ? 0 : FDEV_REMOTE_Y, FDEV_TAG_RECOV);
-            for (int s = 1; s <= fs; s++) {
+            for (int s = 1; s <= fs; s++) { /* the step-s partner's send window, as it left step s - 1 */
                 int pw = c->order[rb_real(x, vdead ^ (1 << s))];
-                void *PW = ftar_buf(c, pw, WS_W);
+                void *PW = ftar_buf(c, pw, rb_acc(x, s - 1));
                 run_reduce(x, at(x, W, dri[s]), at(x, W, dri[s]), at(x, PW, dri[s]), drc[s], FDEV_REMOTE_Y,
                            FDEV_TAG_RECOV);
             }
@@ -216,8 +231,10 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
         int cp = rb_real(x, vdead ^ (1 << fs));
         void *OW = ftar_buf(c, org_w, WS_W);
         if (x->rank == cp && x->corr) { /* :170-180: reduce the window the dead rank owed us */
-            void *W = c->ws[WS_W];
-            run_reduce(x, at(x, W, x->rindex[fs]), at(x, W, x->rindex[fs]), at(x, OW, x->rindex[fs]),
+            /* this rank's step-fs window from its (intact) step fs - 1 input: a pull that was
+             * skipped, cut short or made from a dying rank's memory is simply not used */
+            run_reduce(x, at(x, ftar_local(c, rb_acc(x, fs)), x->rindex[fs]),
+                       at(x, ftar_local(c, rb_acc(x, fs - 1)), x->rindex[fs]), at(x, OW, x->rindex[fs]),
                        x->rcount[fs], FDEV_REMOTE_Y, FDEV_TAG_RECOV);
         }
         if (x->rank == new_entry) { /* :213-241: take over the dead rank's role */
@@ -228,9 +245,18 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
             /* the dead rank's whole reduce-scatter state, not only its current window: a
              * later replay (a second failure) pulls this rank's sindex[s] windows of the
              * steps s <= fs, which all lie in the step-0 window (the reference ships the
-             * whole buffer, :213-241) */
-            void *W = c->ws[WS_W];
-            run_copy(x, at(x, W, dri[0]), at(x, OW, dri[0]), drc[0], FDEV_REMOTE_X, FDEV_TAG_RECOV);
+             * whole buffer, :213-241).  Each part goes where the dead rank held it: the part
+             * of window s it sent at step s + 1 in step s's accumulator, the live window
+             * fs in step fs's (one launch) */
+            fdev_seg seg[MAXSTEPS + 1];
+            int nseg = 0;
+            for (int s = 0; s <= fs; s++) {
+                int64_t off = s < fs ? dsi[s + 1] : dri[fs], n = s < fs ? dsc[s + 1] : drc[fs];
+                if (n <= 0) continue;
+                seg[nseg++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, ftar_local(c, rb_acc(x, s)), off), at(x, OW, off),
+                                         NULL, (size_t)n, NULL, 0};
+            }
+            if (nseg) ftar_run(c, x->dtype, x->op, seg, nseg, FDEV_TAG_RECOV);
             x->has_recov = 0;
         }
         ftar_drain(c);
@@ -669,6 +695,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         return FTAR_ERR_ARG;
     x->adjsize = 1 << x->steps;
     x->rem = c->size - x->adjsize;
+    x->alt = x->rem > 0; /* uniform; fixed for the call (rem only decreases) */
     /* The step-0 copy of the partner's other half (tmp, :191-197) is only ever read by
      * an RS error handler's replay, and every handler aborts before replaying when
      * there is no idle spare (new_entry = 2 rem - 1 = -1, errhandler.c:207-211,377-378).
@@ -830,14 +857,12 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
         }
         /* A partner that dies mid-exchange (after entering, before its side completed) fails
          * the Sendrecv too: the reference then discards the received window (corr, :238-241)
-         * and the RS handler rebuilds it from the impersonator's replay.  The pull reduces in
-         * place, so while a recovery is possible (an idle rank exists; at step 0 the handler
-         * aborts) the window's pre-image is kept in T -- whose half rw0 is unused (T holds
-         * the partner's other half, sw0) -- to undo the reduce.  The pull kernel stores it
-         * itself (rb_plan's save_pre: each stripe's local operand, as read, to T at the same
-         * offset), so the guard costs one extra 16-byte store per vector and no pass of its
-         * own.  If a relay died the window may be partly unreduced, but then a second rank
-         * died with the partner and the handler aborts (nf > 1, errhandler.c:37-38). */
+         * and the RS handler rebuilds it from the impersonator's replay.  With a spare the
+         * step reduced out of place (rb_acc): its input window is intact, so discarding is
+         * just not using the result -- the handler's corr reduce recomputes the window from
+         * the step's input and the replayed state.  (At step 0 the handler aborts.)  If a
+         * relay died the window may be partly unreduced, but then a second rank died with
+         * the partner and the handler aborts (nf > 1, errhandler.c:37-38). */
         int guard = x->rem > 0 && step >= 1 && pw >= 0 && !skip;
         double lb0 = ftar_link_bytes(c);
         int tag = step == 0 ? FDEV_TAG_STEP0 : FDEV_TAG_STEP;
@@ -850,7 +875,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             if (x->vrank != -1 && !skip) {
                 const ftar_pull *pl = P.pull[x->rank];
                 void *PIN = ftar_buf(c, pl[0].src, WS_IN);
-                fdev_seg red = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, W, pl[0].off),
+                fdev_seg red = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, ftar_local(c, pl[0].dst_buf), pl[0].off),
                                 at(x, ftar_local(c, pl[0].x_buf), pl[0].off), at(x, PIN, pl[0].off), (size_t)pl[0].n,
                                 NULL, 0};
                 fdev_seg cpy = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
@@ -869,8 +894,6 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             ftar_xfer_step(c, &P, x->dtype, x->op, tag, skip, FTAR_PH_LOOP, step, NULL, 0, &xs);
         }
         if (guard && !ftar_peer_done(c, pw)) { /* partner died mid-exchange: corr */
-            run_copy(x, at(x, W, x->rindex[step]), at(x, T, x->rindex[step]), x->rcount[step], 0, FDEV_TAG_RECOV);
-            ftar_drain(c);
             x->corr = 1;
             xs.skipped = 1; /* nothing of this window is re-pulled after the agree */
             if (c->verbose)

@@ -77,7 +77,7 @@ static int rd_plan(rd_ctx *x, int distance, int cur, int pred, ftar_plan *P)
         int cr = ftar_comm_rank_of(c, x->active[a]);
         int pw = x->active[a ^ distance];
         ftar_pull *pl = &P->pull[cr][0];
-        *pl = (ftar_pull){FDEV_REDUCE, last, pw, pred >= 0 ? pred : peer_cur(x, pw), 0, 0, 0, (int64_t)x->count, 0, 0};
+        *pl = (ftar_pull){FDEV_REDUCE, last, pw, pred >= 0 ? pred : peer_cur(x, pw), 0, 0, 0, (int64_t)x->count, 0};
         if (a == i) {
             pl->dst_buf = out;
             pl->x_buf = cur;

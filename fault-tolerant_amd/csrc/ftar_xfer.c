@@ -125,14 +125,6 @@ static fdev_seg own_seg(ftar_comm *c, const ftar_pull *pl, int64_t st, int64_t l
     s.kind = pl->kind;
     s.out = at(ftar_local(c, pl->dst_buf), st, es);
     if (pl->to_uout) s.out2 = at(c->uout, st, es);
-    if (pl->save_pre && pl->kind == FDEV_REDUCE && !pl->swap) { /* the in-place reduce's pre-image, same pass */
-        if (pl->to_uout) { /* one second destination per segment: never drop one silently */
-            fprintf(stderr, "ftar: rank %d: a pull both saves its pre-image and writes the output\n", c->wrank);
-            ftar_ctrl_abort(&c->job, FTAR_ERR_STATE);
-        }
-        s.out2 = at(c->ws[WS_T], st, es);
-        s.out2_pre = 1;
-    }
     s.n = (size_t)len;
     if (pl->kind == FDEV_COPY) {
         s.x = pulled;
