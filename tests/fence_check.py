@@ -186,7 +186,7 @@ class Report:
     writes_checked: int = 0
     release: list = field(default_factory=list)
     acquire: list = field(default_factory=list)
-    skipped_dead: int = 0
+    dead_reads: int = 0  # checks against a rank that died before the reader's barrier
 
     @property
     def ok(self) -> bool:
@@ -227,8 +227,17 @@ def check(logs: dict, max_report: int = 20) -> Report:
                 for (x, e, rel, wa, what) in foreign:
                     ax = logs[x].arrive.get(k)
                     if ax is None:
-                        rep.skipped_dead += 1
-                        continue
+                        # X died before barrier k (a recovery reads its memory, or its partner
+                        # pulled its window as it died): what it wrote before its LAST arrival
+                        # must have been released by then, and nothing it wrote after that (its
+                        # in-flight step, which the protocol discards) may be read at all
+                        ax = max(logs[x].arrive.values(), default=-1)
+                        rep.dead_reads += 1
+                        if e > ax and len(rep.release) < max_report:
+                            rep.release.append(f"rank {y} launch {L.n} reads {a.owner}:{a.name}[{a.off}:+{a.n}] after "
+                                               f"barrier {k}, written by rank {x}'s {what} (line {e}) after its last "
+                                               f"arrival (line {ax}) before it died")
+                            continue
                     if e < ax and not rel < ax and len(rep.release) < max_report:
                         rep.release.append(f"rank {y} launch {L.n} reads {a.owner}:{a.name}[{a.off}:+{a.n}] after "
                                            f"barrier {k}; rank {x}'s {what} (line {e}) wrote it and was not released "

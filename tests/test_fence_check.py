@@ -78,3 +78,16 @@ def test_gated_launch_runs_at_its_gate(tmp_path):
     bad[1] = "D sig 0"
     rep = FC.check_prefix(_write(str(tmp_path), {0: rank(0, 1), 1: bad}))
     assert rep.release, rep
+
+
+def test_dead_rank_reads(tmp_path):
+    """A rank that died before the reader's barrier: what it wrote before its last arrival
+    must have been released by then (a recovery reads it: the replay of its step-0 input),
+    and what it wrote after (its in-flight step) must never be read."""
+    dead = ["A 1", "P 1", L(1, w="1:IN:0:64,", sig=1), "D sig 1", "A 2", "P 2", L(2, w="1:W:0:64,")]
+    live = ["A 1", "P 1", "A 2", "P 2", "A 3", "P 3", L(5, r="1:IN:0:64,")]
+    rep = FC.check_prefix(_write(str(tmp_path), {0: live, 1: dead}))
+    assert rep.ok and rep.dead_reads == 1, (rep.release, rep.dead_reads)
+    live[-1] = L(5, r="1:W:0:64,")  # the dead rank's unreleased in-flight step read
+    rep = FC.check_prefix(_write(str(tmp_path), {0: live, 1: dead}))
+    assert rep.release and "after its last arrival" in rep.release[0], rep.release

@@ -50,6 +50,12 @@ BASE = [
     (4, "rd", MIB, {"FTAR_RELAY_MIN": "0"}),               # relayed steps
     (5, "rd", 16384, {}),                                  # pre-step + fan-out
     (4, "raben", 16384, {"FTAR_FLAG_SYNC": "0"}),          # fenced-marker drains only
+    # kills mid-exchange (configs[4]'s shape at 5 ranks = 4 + idle spare): the recovery's
+    # launches -- the impersonator's replay of the dead rank's steps, the corr reduce, the new
+    # entry's state pulls -- read the dead rank's and the survivors' memory across barriers too
+    (5, "raben", MIB, {"FTAR_KILL": "3:1:1:3:1"}),         # RS step 1, DURING, call 1
+    (5, "raben", MIB, {"FTAR_KILL": "4:2:0:3:1"}),         # last AG step, DURING
+    (5, "rd", 16384, {"FTAR_KILL": "1:1:1:3:1"}),          # RD step 1, DURING
     (4, "raben", 64 * MIB, {}),                            # 256 MiB mesh
     (4, "raben", 64 * MIB, {"FTAR_GATE_MAX": str(256 * MIB)}),  # mesh_gated_ag at the headline size
 ]
@@ -64,22 +70,42 @@ CASES = BASE + (WIDE if os.environ.get("FTAR_GPU_FENCE_WIDE") == "1" else [])
 
 def _trace_job(p, algo, n, opts, drop=None, calls=3):
     tmp = tempfile.mkdtemp(prefix="ftar_fence_")
-    env = dict(os.environ, FTBENCH_PATTERN="1", FTAR_TRACE=os.path.join(tmp, "t"), **opts)
-    env.pop("FTAR_KILL", None)
-    env.pop("FTAR_TRACE_DROP", None)
+    # pattern inputs (every element its own exact sum) without kills; rank ids with one
+    env = {k: v for k, v in os.environ.items() if k not in ("FTAR_KILL", "FTAR_TRACE_DROP")}
+    env.update(opts, FTBENCH_PATTERN="0" if "FTAR_KILL" in opts else "1", FTAR_TRACE=os.path.join(tmp, "t"))
     if drop:
         env["FTAR_TRACE_DROP"] = drop
     cp = subprocess.run([os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ",".join("0" * p),
                          os.path.join(H.PKG, "bin", "ftbench"), algo, str(n), str(calls)], env=env,
                         capture_output=True, text=True, timeout=240)
-    assert cp.returncode == 0, cp.stderr[-2000:]
     lines = [json.loads(ln) for ln in cp.stdout.splitlines() if ln.startswith("{")]
-    assert sorted(ln["rank"] for ln in lines) == list(range(p)), cp.stdout[-1000:]
-    for ln in lines:
-        assert all(c["rc"] == 0 and c["uniform"] for c in ln["calls"]), ln
     logs = FC.load(os.path.join(tmp, "t"))
     assert sorted(logs) == list(range(p))
-    return FC.check(logs), logs
+    if "FTAR_KILL" not in opts:
+        assert cp.returncode == 0, cp.stderr[-2000:]
+        assert sorted(ln["rank"] for ln in lines) == list(range(p)), cp.stdout[-1000:]
+        for ln in lines:
+            assert all(c["rc"] == 0 and c["uniform"] for c in ln["calls"]), ln
+        return FC.check(logs), logs
+    # a kill: the victim is gone, every survivor completed every call, all with the same
+    # value per call (inputs are the rank ids), and the comm shrank by one; Raben's kill call
+    # keeps the victim's contribution (the impersonator's replay), later calls are the
+    # survivors' sum
+    victim = int(opts["FTAR_KILL"].split(":")[0])
+    assert "dies mid-exchange" in cp.stderr, cp.stderr[-2000:]
+    assert sorted(ln["rank"] for ln in lines) == [r for r in range(p) if r != victim], cp.stdout[-1000:]
+    full, rest = float(sum(range(p))), float(sum(range(p)) - victim)
+    for ln in lines:
+        cs = ln["calls"]
+        assert all(c["rc"] == 0 and c["uniform"] for c in cs), ln
+        assert [c["value"] for c in cs] == [c["value"] for c in lines[0]["calls"]], (ln, lines[0])
+        assert cs[0]["value"] == full and cs[-1]["value"] == rest, ln
+        if algo == "raben":
+            assert cs[1]["value"] == full, ln
+        assert cs[1]["recoveries"] == 1 and cs[-1]["comm_size"] == p - 1, ln
+    rep = FC.check(logs)
+    assert rep.dead_reads > 0  # the recovery read the dead rank's memory, and that was checked
+    return rep, logs
 
 
 @pytest.mark.timeout(300)
