@@ -104,7 +104,10 @@ def _trace_job(p, algo, n, opts, drop=None, calls=3):
             assert cs[1]["value"] == full, ln
         assert cs[1]["recoveries"] == 1 and cs[-1]["comm_size"] == p - 1, ln
     rep = FC.check(logs)
-    assert rep.dead_reads > 0  # the recovery read the dead rank's memory, and that was checked
+    if algo == "raben" and opts["FTAR_KILL"].split(":")[1] == "1":
+        # the reduce-scatter replay read the dead rank's step-0 input where it lies (one GPU:
+        # the copy is elided), and that read was checked against the dead rank's releases
+        assert rep.dead_reads > 0
     return rep, logs
 
 
