@@ -253,8 +253,8 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
             for (int s = 0; s <= fs; s++) {
                 int64_t off = s < fs ? dsi[s + 1] : dri[fs], n = s < fs ? dsc[s + 1] : drc[fs];
                 if (n <= 0) continue;
-                seg[nseg++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, ftar_local(c, rb_acc(x, s)), off), at(x, OW, off),
-                                         NULL, (size_t)n, NULL, 0};
+                seg[nseg++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, ftar_local(c, rb_acc(x, s)), off),
+                                         at(x, OW, off), NULL, (size_t)n, NULL, 0};
             }
             if (nseg) ftar_run(c, x->dtype, x->op, seg, nseg, FDEV_TAG_RECOV);
             x->has_recov = 0;
