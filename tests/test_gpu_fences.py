@@ -34,6 +34,7 @@ BASE = [
     (4, "raben", 262148, {}),                              # 1 MiB + 16 B: two-launch mesh, read in place
     (4, "raben", MIB, {}),                                 # 4 MiB mesh
     (4, "raben", MIB, {"FTAR_TREE_UNROLL": "2"}),          # mesh_u2
+    (8, "raben", MIB, {"FTAR_TREE_UNROLL": "4"}),          # mesh_u4, 8 ranks
     (4, "raben", MIB, {"FTAR_PUSH": "1"}),                 # mesh_push
     (4, "raben", MIB, {"FTAR_PUSH": "2"}),                 # mesh_push2
     (4, "raben", 16384, {"FTAR_PUSH": "2", "FTAR_ONESHOT_MAX": "0"}),
@@ -61,7 +62,7 @@ BASE = [
 ]
 WIDE = [
     (8, "raben", 1, {}), (8, "raben", 16384, {}), (8, "raben", 262140, {}), (8, "raben", 262148, {}),
-    (8, "raben", MIB, {"FTAR_TREE_UNROLL": "4"}), (8, "raben", MIB, {"FTAR_PUSH": "2"}),
+    (8, "raben", MIB, {}), (8, "raben", MIB, {"FTAR_PUSH": "2"}),
     (8, "raben", MIB, {"FTAR_MESH": "0", "FTAR_RELAY_MIN": "0"}), (8, "rd", MIB, {"FTAR_RELAY_MIN": "0"}),
     (8, "rd", 16384, {}), (2, "rd", 262148, {}), (2, "raben", 64 * MIB, {}), (8, "raben", 64 * MIB, {}),
 ]
