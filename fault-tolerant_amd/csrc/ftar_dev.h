@@ -98,10 +98,11 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
 #define FDEV_MAX_TREE 16
 int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
               size_t n, int tag);
-/* The same tree, its result also stored to `nmore` (<= 7) further destinations -- peer
- * mappings (the push mesh's allgather: the owner's block into every peer). */
+/* The same tree, its result also stored to `nmore` (<= 7) further destinations: peer
+ * mappings when `more_remote` (the push mesh's allgather: the owner's block into every peer),
+ * else this device's memory (the caller's rbuf; byte accounting only). */
 int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
-                  void *const *more, int nmore, size_t n, int tag);
+                  void *const *more, int nmore, int more_remote, size_t n, int tag);
 /* ntree (<= FDEV_MAX_BATCH) trees of nsrc (2, 4 or 8) sources in ONE launch: tree t
  * reduces src[t * nsrc + j], j < nsrc, into out[t] over n[t] elements (remote_mask[t] as
  * in fdev_tree).  Meant for small vectors: a tree beyond the device's workgroup budget

@@ -704,11 +704,11 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
 int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
               size_t n, int tag)
 {
-    return fdev_tree_out(d, dtype, op, src, nsrc, remote_mask, out, nullptr, 0, n, tag);
+    return fdev_tree_out(d, dtype, op, src, nsrc, remote_mask, out, nullptr, 0, 0, n, tag);
 }
 
 int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
-                  void *const *more, int nmore, size_t n, int tag)
+                  void *const *more, int nmore, int more_remote, size_t n, int tag)
 {
     size_t es = esize_of(dtype);
     if (es == 0 || op < 0 || op >= ftar::kNumOps || tag < 0 || tag >= FDEV_NTAGS ||
@@ -718,8 +718,9 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
     }
     if (n == 0) return 0;
     int nremote = __builtin_popcount(remote_mask & ((1u << nsrc) - 1));
-    d->ctr.link_bytes += (double)n * (double)es * (nremote + nmore); // extra destinations: peers' HBM
-    d->ctr.hbm_bytes += (double)n * (double)es * (nsrc - nremote + 1);
+    const int mr = more_remote ? nmore : 0; // extra destinations in peers' HBM, or in ours
+    d->ctr.link_bytes += (double)n * (double)es * (nremote + mr);
+    d->ctr.hbm_bytes += (double)n * (double)es * (nsrc - nremote + 1 + nmore - mr);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
         e0 = get_event(d);

@@ -56,6 +56,7 @@ typedef struct {
     int push;       /* the mesh's reduce-scatter by remote stores into the owners' R (FTAR_OPT_PUSH) */
     int64_t slot;   /* push: elements per source slot in an owner's R */
     int oneshot;    /* mesh of a small vector: every block in its owner's tree, one launch */
+    int own_in_rbuf; /* the mesh's tree stored this rank's final block in rbuf too: the allgather skips it */
     /* the one-shot launch queued ahead of the barrier (rb_oneshot_prelaunch): its plan, to
      * be checked against the one the inputs' resolution gives */
     int gated;
@@ -393,7 +394,7 @@ static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf, void *rbuf)
         for (int j = 1; j < p; j++) more[nmore++] = at(x, ftar_buf(c, c->order[rb_real(x, v ^ j)], WS_W), own0);
     }
     void *out = x->push == 2 ? at(x, rbuf, own0) : at(x, W, own0);
-    if (fdev_tree_out(c->dev, x->dtype, x->op, src, p, 0, out, more, nmore, (size_t)own_n, FDEV_TAG_STEP)) {
+    if (fdev_tree_out(c->dev, x->dtype, x->op, src, p, 0, out, more, nmore, 1, (size_t)own_n, FDEV_TAG_STEP)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
@@ -470,8 +471,9 @@ static int rb_mesh_ag_segs(rb_ctx *x, void *rbuf, fdev_seg *segs)
     ftar_comm *c = x->c;
     const int L = x->steps, p = x->adjsize, v = x->vrank;
     int ns = 0;
-    segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, x->rindex[L - 1]), at(x, c->ws[WS_W], x->rindex[L - 1]), NULL,
-                            (size_t)x->rcount[L - 1], NULL, 0};
+    if (!x->own_in_rbuf)
+        segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, x->rindex[L - 1]), at(x, c->ws[WS_W], x->rindex[L - 1]),
+                                NULL, (size_t)x->rcount[L - 1], NULL, 0};
     for (int j = 1; j < p; j++) {
         int u = v ^ j;
         int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
@@ -511,7 +513,17 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
     }
     double lb0 = ftar_link_bytes(c);
     ftar_note_launch(c, src[1], (size_t)own_n * x->es);
-    if (fdev_tree(c->dev, x->dtype, x->op, src, p, remote, at(x, W, own0), (size_t)own_n, FDEV_TAG_STEP0)) {
+    /* the block goes to W, where the peers' allgather pulls it, and in the same pass to its
+     * place in rbuf (a second destination of the tree: one more local store of S/p), so the
+     * allgather only pulls the peers' blocks -- no local copy of this rank's own block, S/p
+     * fewer HBM reads per call (in place, rbuf's block is sbuf's, read by this lane only) */
+    void *own_out = at(x, rbuf, own0);
+    /* only where rbuf is co-aligned with W (a 16-byte vector body needs every operand at the
+     * same offset mod 16; otherwise the tree would fall back to scalar accesses): else the
+     * allgather copies the block out of W as before */
+    x->own_in_rbuf = (((uintptr_t)own_out ^ (uintptr_t)at(x, W, own0)) & 15) == 0;
+    if (fdev_tree_out(c->dev, x->dtype, x->op, src, p, remote, at(x, W, own0), &own_out, x->own_in_rbuf, 0,
+                      (size_t)own_n, FDEV_TAG_STEP0)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }

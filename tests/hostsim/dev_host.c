@@ -302,16 +302,16 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
     } while (0)
 
 int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
-                  void *const *more, int nmore, size_t n, int tag);
+                  void *const *more, int nmore, int more_remote, size_t n, int tag);
 
 int fdev_tree(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
               size_t n, int tag)
 {
-    return fdev_tree_out(d, dtype, op, src, nsrc, remote_mask, out, NULL, 0, n, tag);
+    return fdev_tree_out(d, dtype, op, src, nsrc, remote_mask, out, NULL, 0, 0, n, tag);
 }
 
 int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int nsrc, unsigned remote_mask, void *out,
-                  void *const *more, int nmore, size_t n, int tag)
+                  void *const *more, int nmore, int more_remote, size_t n, int tag)
 {
     if (!(nsrc == 2 || nsrc == 4 || nsrc == 8 || nsrc == 16)) return 13;
     if (d->gate_pending) fdev_gate_open(d, 1);
@@ -322,7 +322,7 @@ int fdev_tree_out(ftar_dev *d, int dtype, int op, const void *const *src, int ns
     default: TREE(double, op_f64); break;
     }
     for (int o = 0; o < nmore; o++) memcpy(more[o], out, n * esz(dtype));
-    d->ctr.link_bytes += (double)n * (double)esz(dtype) * (__builtin_popcount(remote_mask) + nmore);
+    d->ctr.link_bytes += (double)n * (double)esz(dtype) * (__builtin_popcount(remote_mask) + (more_remote ? nmore : 0));
     d->ctr.launches[tag]++;
     return 0;
 }
