@@ -14,6 +14,7 @@ removed acquire (FTAR_TRACE_DROP=acquire) must each fail it.
 FTAR_GPU_FENCE_WIDE=1 adds the 8-rank and remaining size/form combinations."""
 import json
 import os
+import shutil
 import subprocess
 import tempfile
 
@@ -81,6 +82,7 @@ def _trace_job(p, algo, n, opts, drop=None, calls=3):
                         capture_output=True, text=True, timeout=240)
     lines = [json.loads(ln) for ln in cp.stdout.splitlines() if ln.startswith("{")]
     logs = FC.load(os.path.join(tmp, "t"))
+    shutil.rmtree(tmp, ignore_errors=True)
     assert sorted(logs) == list(range(p))
     if "FTAR_KILL" not in opts:
         assert cp.returncode == 0, cp.stderr[-2000:]
