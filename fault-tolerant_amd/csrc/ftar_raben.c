@@ -394,11 +394,17 @@ static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf, void *rbuf)
         for (int j = 1; j < p; j++) more[nmore++] = at(x, ftar_buf(c, c->order[rb_real(x, v ^ j)], WS_W), own0);
     }
     void *out = x->push == 2 ? at(x, rbuf, own0) : at(x, W, own0);
-    if (fdev_tree_out(c->dev, x->dtype, x->op, src, p, 0, out, more, nmore, 1, (size_t)own_n, FDEV_TAG_STEP)) {
+    if (x->push == 1) { /* as the pull form: the block into rbuf too, where co-aligned (rb_mesh) */
+        more[0] = at(x, rbuf, own0);
+        x->own_in_rbuf = (((uintptr_t)more[0] ^ (uintptr_t)out) & 15) == 0;
+        nmore = x->own_in_rbuf;
+    }
+    if (fdev_tree_out(c->dev, x->dtype, x->op, src, p, 0, out, more, nmore, x->push == 2, (size_t)own_n,
+                      FDEV_TAG_STEP)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
-    ftar_note_launch(c, nmore ? more[0] : NULL, 0);
+    ftar_note_launch(c, x->push == 2 ? more[0] : NULL, 0);
     if (x->push == 2) {
         ftar_launched(c, FTAR_PH_AG, L - 1);
         for (int s = L - 2; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_DURING);
