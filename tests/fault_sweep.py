@@ -57,7 +57,8 @@ def main():
     ap.add_argument("--aborts", action="store_true", help="also run the draws the oracle aborts (must abort)")
     a = ap.parse_args()
     rnd = random.Random(a.seed)
-    pts = [(v, ph, st, pt) for v in range(a.p) for ph in (1, 2) for st in range(3) for pt in range(4)]
+    nst = max(3, a.p.bit_length() - 1)  # every step of the schedule (L = floor(log2 p)), at least 3
+    pts = [(v, ph, st, pt) for v in range(a.p) for ph in (1, 2) for st in range(nst) for pt in range(4)]
     cases = []
     for algo in ("raben", "rd"):
         for _ in range(a.draws):
