@@ -181,8 +181,11 @@ def pmc_live(args, kernel, steps=20, timeout=90.0):
             rc, out, err, to = run_proc(cmd, timeout)
             info["passes"][ctr] = {"rc": rc, "s": round(time.monotonic() - t0, 1), "timed_out": to}
             files = [os.path.join(r, n) for r, _, fs in os.walk(d) for n in fs if n.endswith("counter_collection.csv")]
-            v = [float(row["Counter_Value"]) for fp in files for row in csv.DictReader(open(fp))
-                 if row["Counter_Name"] == ctr and kernel in row["Kernel_Name"]]
+            v = []
+            for fp in files:
+                with open(fp, newline="") as f:
+                    v += [float(row["Counter_Value"]) for row in csv.DictReader(f)
+                          if row["Counter_Name"] == ctr and kernel in row["Kernel_Name"]]
             if rc != 0 or to or not v:
                 info["error"] = f"{ctr}: rc {rc}, timed out {to}, {len(v)} dispatches; {err[-300:]}"
                 return None, info
