@@ -9,6 +9,9 @@ This sweep found the new-entry state hand-off and the BARRIER co-victim wait (DE
 §3, "Second failure after a promotion").
 
 usage: python tests/fault_sweep.py [--p 11] [--kills 2] [--draws 400] [--seed 3] [--jobs 6] [--aborts]
+                                  [--spread 8] [--withdraw]
+--spread K puts rank r on device r % K (the node's layout: the auto redundancy moves Raben's
+step-0 copy), --withdraw has each victim retract its input as it dies (a lost device's memory).
 """
 import argparse
 import os
@@ -25,7 +28,7 @@ import harness as H  # noqa: E402
 import oracle as O  # noqa: E402
 
 
-def run_one(algo, p, op, kills, count, aborts=False):
+def run_one(algo, p, op, kills, count, aborts=False, devmap=None, env=None):
     ins = H.with_specials(O.random_inputs(p, count, seed=p + 78), p + 4)
     fn = O.rabenseifner if algo == "raben" else O.recursive_doubling
     o = fn(ins, list(kills), op=op)
@@ -34,7 +37,7 @@ def run_one(algo, p, op, kills, count, aborts=False):
     if not o.aborted and sum(s == O.DEAD for s in o.status) < len(kills):
         return None
     try:
-        r = H.run_probe(algo, ins, list(kills), op=op, backend="hostsim", timeout=30)
+        r = H.run_probe(algo, ins, list(kills), op=op, backend="hostsim", timeout=30, devmap=devmap, env_extra=env)
     except Exception:
         return "hang"
     if o.aborted:  # the product must abort too (MPI_Abort line, no survivor output)
@@ -55,6 +58,8 @@ def main():
     ap.add_argument("--count", type=int, default=1031)
     ap.add_argument("--jobs", type=int, default=6)
     ap.add_argument("--aborts", action="store_true", help="also run the draws the oracle aborts (must abort)")
+    ap.add_argument("--spread", type=int, default=0, help="rank r on device r %% K (0: every rank on device 0)")
+    ap.add_argument("--withdraw", action="store_true", help="victims retract their input as they die")
     a = ap.parse_args()
     rnd = random.Random(a.seed)
     nst = max(3, a.p.bit_length() - 1)  # every step of the schedule (L = floor(log2 p)), at least 3
@@ -66,7 +71,9 @@ def main():
             if len({k[0] for k in ks}) == a.kills:
                 cases.append((algo, a.p, rnd.choice([0, 2, 3]), ks, a.count))
     with ThreadPoolExecutor(a.jobs) as ex:
-        res = list(ex.map(lambda c: run_one(*c, aborts=a.aborts), cases))
+        devmap = ",".join(str(r % a.spread) for r in range(a.p)) if a.spread > 0 else None
+        env = {"FTAR_KILL_WITHDRAW": "1"} if a.withdraw else None
+        res = list(ex.map(lambda c: run_one(*c, aborts=a.aborts, devmap=devmap, env=env), cases))
     ran = [(c, r) for c, r in zip(cases, res) if r is not None]
     bad = [(c, r) for c, r in ran if r != "ok"]
     what = "recovering or aborting" if a.aborts else "recovering"

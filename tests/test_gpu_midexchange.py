@@ -223,6 +223,57 @@ def test_random_two_kills_gpu(oracle, seed):
         n += 1
 
 
+# The node's recovery shape: ranks on 8 GPUs make the auto redundancy move Raben's step-0
+# copy (FTAR_REDUNDANCY=1 here, where every rank shares GPU 0), and a victim's HBM may go
+# with it (FTAR_KILL_WITHDRAW: its workspace generation moves on and its send buffer is
+# retracted, so any plan that would read it refuses).  On one GPU a dead process's mapping
+# stays readable, so only this makes a recovery that still reads it fail here.
+NODE_SHAPE = {"FTAR_REDUNDANCY": "1", "FTAR_KILL_WITHDRAW": "1"}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("algo,p,kill", [("raben", 9, (6, 1, 1, 3)), ("raben", 9, (3, 1, 2, 3)),
+                                         ("raben", 9, (6, 2, 1, 3)), ("raben", 9, (8, 2, 0, 3)),
+                                         ("raben", 5, (3, 1, 1, 3)), ("rd", 6, (1, 1, 1, 3)),
+                                         ("rd", 8, (5, 1, 2, 3))])
+def test_node_shape_recovery_reads_no_dead_memory(oracle, algo, p, kill):
+    """Recoveries in the node's shape (step-0 copy moved, the victim's memory withdrawn as it
+    dies): RS steps 1 / 2 replayed from the partner's copy, AG kills served by the original
+    partner, RD's shrink and spare branches -- bit-exact against the oracle (MAX over NaN /
+    signed zeros pins the recovery path), none refused for a dead rank's input (the host-sim
+    draws thousands of these: tests/fault_sweep.py --spread 8 --withdraw)."""
+    fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+    ins = H.with_specials(oracle.random_inputs(p, (1 << 20) + 3, seed=800 + kill[0]), p)
+    o, r = _check(fn, algo, ins, [kill], op=2, env=NODE_SHAPE)
+    assert not o.aborted and o.status[kill[0]] == oracle.DEAD
+    assert "withdraws its input" in r.stderr and "not readable" not in r.stderr, r.stderr[-1500:]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", _seeds("FTAR_GPU_NODE_SHAPE_SEEDS", [0]))
+def test_node_shape_random_kills(oracle, seed):
+    """Random single and double kills in the node's shape (NODE_SHAPE), Raben p = 5 / 9 / 11
+    and RD p = 6 / 8: outcome class and every survivor's bits as the oracle's."""
+    import random
+    rng = random.Random(2000 + seed)
+    n = 0
+    while n < (8 if H.WIDE else 4):
+        algo = rng.choice(["raben", "rd"])
+        p = rng.choice([5, 9, 11] if algo == "raben" else [6, 8])
+        pts = [(v, ph, st, pt) for v in range(p) for ph in ((1, 2) if algo == "raben" else (1,))
+               for st in range(3) for pt in (3, 3, 0, 1, 2)]
+        kills = rng.sample(pts, rng.choice([1, 2]))
+        if len({k[0] for k in kills}) < len(kills):
+            continue
+        fn = oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling
+        ins = H.with_specials(oracle.random_inputs(p, (1 << 18) + 3, seed=seed * 100 + n), p)
+        o = fn(ins, kills, op=2)
+        if o.aborted or sum(st == oracle.DEAD for st in o.status) < len(kills):
+            continue  # recoveries only: an abort shows nothing about the memory they read
+        _check(fn, algo, ins, kills, op=2, env=NODE_SHAPE)
+        n += 1
+
+
 from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
 
 GPU_TRANSPORTS = [{}, {"FTAR_RELAY_MIN": "0", "FTAR_MESH": "0"}, {"FTAR_COPY_ENGINE": "1", "FTAR_RELAY": "0"},

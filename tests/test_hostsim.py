@@ -963,3 +963,30 @@ def test_redundancy_auto_uses_physical_device_ids(hostsim, oracle):
     for w, s in enumerate(o.status):
         if s == 0:
             assert np.array_equal(r.outputs[w][0].view(np.uint32), o.outputs[w].view(np.uint32)), w
+
+
+def test_node_layout_random_kills_never_read_dead_memory(hostsim):
+    """The node's layout (rank r on device r % 8: the auto redundancy moves Raben's step-0
+    copy) with every victim withdrawing its memory as it dies (FTAR_KILL_WITHDRAW, a lost
+    device): random single and double kills at p = 9 / 11 (Raben with spares) and 6 / 8 (RD)
+    recover or abort exactly as the oracle, so no recovery path reads a dead rank's HBM
+    (`tests/fault_sweep.py --spread 8 --withdraw` draws thousands; profiles/r05/sweeps)."""
+    import random
+    import fault_sweep as FS
+    rnd = random.Random(5)
+    ran = 0
+    for _ in range(60):
+        algo = rnd.choice(["raben", "rd"])
+        p = rnd.choice([9, 11] if algo == "raben" else [6, 8])
+        pts = [(v, ph, st, pt) for v in range(p) for ph in (1, 2) for st in range(3) for pt in range(4)]
+        ks = tuple(rnd.sample(pts, rnd.choice([1, 2])))
+        if len({k[0] for k in ks}) < len(ks):
+            continue
+        devmap = ",".join(str(r % 8) for r in range(p))
+        res = FS.run_one(algo, p, rnd.choice([0, 2, 3]), ks, 257, aborts=True, devmap=devmap,
+                         env={"FTAR_KILL_WITHDRAW": "1"})
+        if res is None:
+            continue
+        assert res == "ok", (algo, p, ks, res)
+        ran += 1
+    assert ran >= 30, ran
