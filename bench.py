@@ -996,7 +996,7 @@ def multi(args):
         dist.barrier()
         sync()
         t0 = time.perf_counter()
-        step0 = kern = syncw = drain = gl = gh = 0.0
+        step0 = kern = syncw = drain = gl = gh = pw = 0.0
         for _ in range(steps):
             fn()
             st = comm.last_stats()
@@ -1006,10 +1006,11 @@ def multi(args):
             drain += st.drain_s
             gl += st.gated_launches - st.gated_skips
             gh += st.gate_holds
+            pw += st.peer_waits - st.peer_wait_skips
         sync()
         t1 = time.perf_counter()
         dist.barrier()
-        t, k, kall, sw, dr, gl, gh = max_over_ranks([t1 - t0, step0, kern, syncw, drain, gl, gh])
+        t, k, kall, sw, dr, gl, gh, pw = max_over_ranks([t1 - t0, step0, kern, syncw, drain, gl, gh, pw])
         timed.link_bytes = comm.last_stats().step0_link_bytes
         # where a call's time goes (max over ranks of each part, per call)
         timed.breakdown = {"call_ms": round(t / steps * 1e3, 4), "kernels_ms": round(kall / steps, 4),
@@ -1018,7 +1019,9 @@ def multi(args):
                            # gated launches that ran, and those given up at a barrier that waited
                            # past FTAR_GATE_HOLD_US (max over ranks, all timed calls): a gated row
                            # mostly given up measures the hold, not the gate
-                           "gated_launches": int(gl), "gate_holds": int(gh)}
+                           "gated_launches": int(gl), "gate_holds": int(gh),
+                           # allgathers ordered behind the peers' trees on the device (FTAR_OPT_MESH_WAIT)
+                           "peer_waits": int(pw)}
         return t / steps, k / steps
 
     def timed_split(fn):
@@ -1053,8 +1056,9 @@ def multi(args):
         return timed(fn, steps, warmup)[0]
 
     opts = (ftar.OPT_RELAY, ftar.OPT_OVERLAP, ftar.OPT_COPY_ENGINE, ftar.OPT_REDUNDANCY, ftar.OPT_MESH, ftar.OPT_PUSH,
-            ftar.OPT_TREE_UNROLL)
-    pads = (0, 0, 0, 0, 0, 0, 1)  # PUSH off and one vector per tree lane unless named
+            ftar.OPT_TREE_UNROLL, ftar.OPT_MESH_WAIT)
+    # PUSH off, one vector per tree lane and the allgather ordered on the device unless named
+    pads = (0, 0, 0, 0, 0, 0, 1, 1)
     defaults = {o: comm.get_option(o) for o in opts}
     gmax_lib = comm.get_option(ftar.OPT_GATE_MAX)  # the library's mid-size gate limit (1 MiB)
 
@@ -1116,17 +1120,23 @@ def multi(args):
             cands["mesh_push"] = (1, 1, 1, 1, g0)  # remote stores in the reduce-scatter
             if world <= 8:
                 cands["mesh_push2"] = (1, 1, 2, 1, g0)  # ... and in the allgather
+            if world > 2:
+                # the allgather after a host agree round, as before the device-side wait
+                # (FTAR_OPT_MESH_WAIT=0): the node times the agree the default form leaves out
+                cands["mesh_host_ag"] = (1, 1, 0, 1, g0, 0)
             if world > 2 and comm.get_option(ftar.OPT_GATE):
                 # the allgather's launch queued behind the tree at this size too (FTAR_OPT_GATE_MAX
                 # >= S), its gate opened by the reduce-scatter's agree: the launch latency after
                 # the barrier leaves the call's non-kernel time.  On one
                 # GPU shared by the ranks the waiting launch holds CUs the others need (DESIGN.md
                 # 6); with one rank per GPU nothing else competes -- the node decides
-                cands["mesh_gated_ag"] = (1, 1, 0, 1, max(float(S), g0))
+                cands["mesh_gated_ag"] = (1, 1, 0, 1, max(float(S), g0), 0)
         if world >= 3 and comm.get_option(ftar.OPT_RELAY):
             cands["relay2hop"] = (0, 1, 0, 1, g0)
         cands["direct"] = (0, 0, 0, 1, g0)
-        sel_opts = (ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH, ftar.OPT_TREE_UNROLL, ftar.OPT_GATE_MAX)
+        sel_opts = (ftar.OPT_MESH, ftar.OPT_RELAY, ftar.OPT_PUSH, ftar.OPT_TREE_UNROLL, ftar.OPT_GATE_MAX,
+                    ftar.OPT_MESH_WAIT)
+        cands = {k: tuple(v) + (1,) * (len(sel_opts) - len(v)) for k, v in cands.items()}
         if len(cands) > 1:
             times, inexact, failed = {}, [], {}
             for name, vals in cands.items():
@@ -1164,9 +1174,11 @@ def multi(args):
     # the headline's allgather queued behind the tree (mesh_gated_ag): counted in the plain pass
     # (the profiled pass gates nothing: kernel events would time the wait)
     gated_ag = meshed and not oneshot and not pushed and breakdown.get("plain_gated_launches", 0) > 0
+    # the allgather after a host agree round (FTAR_OPT_MESH_WAIT=0) instead of the device wait
+    host_ag = meshed and not oneshot and not pushed and not gated_ag and comm.last_stats().peer_waits == 0
     transport = "mesh-oneshot" if oneshot else ("mesh-push2" if push_opt == 2 and world <= 8 else "mesh-push") \
-        if pushed else "mesh-gated-ag" if gated_ag else (f"mesh-u{unroll}" if unroll > 1 else "mesh") if meshed \
-        else "relay2hop" if relayed else "direct"
+        if pushed else "mesh-gated-ag" if gated_ag else "mesh-host-ag" if host_ag else \
+        (f"mesh-u{unroll}" if unroll > 1 else "mesh") if meshed else "relay2hop" if relayed else "direct"
     keep = bool(comm.last_stats().step0_copy)  # the headline call moved the reference's step-0 copy
     chosen_opts = {o: comm.get_option(o) for o in opts}
     # the headline's gate limit (S when mesh_gated_ag was chosen); every later leg runs at the
@@ -1225,7 +1237,11 @@ def multi(args):
         "mesh-oneshot": "Rabenseifner, one-shot mesh: every block in its owner's reduction tree in one launch "
                         "(power-of-two p, no spare)",
         "mesh": "Rabenseifner, one-hop mesh: reduce-scatter as one tree kernel over p-1 peer pulls, allgather as "
-                "one multi-source pull (power-of-two p, no spare; same reduction tree as recursive halving)",
+                "one multi-source pull queued right behind it and ordered on the device (each rank publishes a flag "
+                "in its HBM once its tree is released; the allgather waits for the peers' flags, no host agree in "
+                "between) (power-of-two p, no spare; same reduction tree as recursive halving)",
+        "mesh-host-ag": "Rabenseifner, one-hop mesh, the allgather launched after the reduce-scatter's host agree round "
+                        "(FTAR_OPT_MESH_WAIT=0; power-of-two p, no spare)",
         "mesh-u2": "Rabenseifner, one-hop mesh, tree kernel with 2 vectors per lane and source (more remote loads in "
                    "flight), allgather as one multi-source pull (power-of-two p, no spare; same tree)",
         "mesh-u4": "Rabenseifner, one-hop mesh, tree kernel with 4 vectors per lane and source (more remote loads in "
@@ -1401,8 +1417,9 @@ def multi(args):
             if pow2 and world > 2:
                 # the allgather queued behind the tree at the job's size (transport selection's
                 # mesh_gated_ag)
-                checks.append(("mesh_gated_ag", (1, 1, 0, 0, 1), raben_fn, None,
+                checks.append(("mesh_gated_ag", (1, 1, 0, 0, 1, 0, 1, 0), raben_fn, None,
                                {ftar.OPT_GATE_MAX: max(float(S), gmax_lib)}))
+                checks.append(("mesh_host_ag", (1, 1, 0, 0, 1, 0, 1, 0), raben_fn, None, {}))
             if pow2:
                 checks += [(name, vals, raben_fn, min(16384, args.count), {}) for name, vals in
                            (("mesh_push_64KiB", (1, 1, 0, 0, 1, 1)), ("mesh_push2_64KiB", (1, 1, 0, 0, 1, 2)),
@@ -1513,7 +1530,8 @@ def multi(args):
         # the partner's window + a local reduce kernel; relay_full_exchange: the relay with
         # the reference's step-0 full exchange.  Each variant records its own failure.
         out = {}
-        variants = (("mesh", (1, 1, 0, 0, 1)), ("mesh_gated_ag", (1, 1, 0, 0, 1)),
+        variants = (("mesh", (1, 1, 0, 0, 1)), ("mesh_host_ag", (1, 1, 0, 0, 1, 0, 1, 0)),
+                    ("mesh_gated_ag", (1, 1, 0, 0, 1, 0, 1, 0)),
                     ("mesh_push", (1, 1, 0, 0, 1, 1)), ("mesh_push2", (1, 1, 0, 0, 1, 2)),
                     ("relay2hop", (1, 1, 0, 0, 0)),
                     ("direct", (0, 1, 0, 0, 0)), ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
@@ -1527,13 +1545,18 @@ def multi(args):
                     continue
                 if name == "mesh_gated_ag" and (world == 2 or not comm.get_option(ftar.OPT_GATE)):
                     continue
+                if name == "mesh_host_ag" and world == 2:
+                    continue
                 try:
                     maybe_fail(f"transports:{name}")
                     set_opts(vals)
-                    if name == "mesh_gated_ag":
-                        comm.set_option(ftar.OPT_GATE_MAX, max(float(S), gmax_lib))
-                    tv, kv = timed_split(raben)
-                    comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)
+                    # every variant starts from the library's gate limit: a variant that raised
+                    # with the allgather gated must not leave it on for the next rows
+                    comm.set_option(ftar.OPT_GATE_MAX, max(float(S), gmax_lib) if name == "mesh_gated_ag" else gmax_lib)
+                    try:
+                        tv, kv = timed_split(raben)
+                    finally:
+                        comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)
                     lb = timed.link_bytes
                     tv_rd = timed(rd)[0] if name in ("relay2hop", "direct", "copy_engine") else None
                     out[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2),

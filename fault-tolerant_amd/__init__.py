@@ -32,6 +32,7 @@ OPT_GATE = 9
 OPT_FLAG_SYNC = 10
 OPT_TREE_UNROLL = 11
 OPT_GATE_MAX = 12
+OPT_MESH_WAIT = 13
 REDUNDANCY_NEVER, REDUNDANCY_ALWAYS, REDUNDANCY_AUTO = 0, 1, 2  # OPT_REDUNDANCY values
 SUCCESS, ERR_ARG, ERR_UNKNOWN, ERR_OTHER, ERR_PROC_FAILED = 0, 13, 14, 16, 75
 ERR_OP = 9  # MPI_ERR_OP: a logical / bitwise op on a float type
@@ -51,7 +52,7 @@ class Stats(ctypes.Structure):
                 ("mesh_steps", ctypes.c_int), ("export_retries", ctypes.c_int),
                 ("gated_launches", ctypes.c_int), ("gated_skips", ctypes.c_int),
                 ("user_stream_waits", ctypes.c_int), ("step0_copy", ctypes.c_int), ("gate_holds", ctypes.c_int),
-                ("gate_relaunches", ctypes.c_int)]
+                ("gate_relaunches", ctypes.c_int), ("peer_waits", ctypes.c_int), ("peer_wait_skips", ctypes.c_int)]
 
 
 class Kill(ctypes.Structure):

@@ -263,6 +263,9 @@ def decisions(line: dict) -> dict:
         # the allgather queued behind the tree at the headline size
         "gated_ag_faster": (times["mesh_gated_ag"] < times["mesh"]) if "mesh_gated_ag" in times and "mesh" in times
         else None,
+        # the allgather ordered on the device (the default) vs after a host agree (FTAR_OPT_MESH_WAIT=0)
+        "device_wait_faster": (times["mesh"] < times["mesh_host_ag"]) if "mesh_host_ag" in times and "mesh" in times
+        else None,
         "gate_max_bytes": gate_max,
         "gate_max_changes": gate_max != (1 << 20),
         "all_exact": ex.get("all_exact"),

@@ -113,16 +113,19 @@ void ftar_maybe_die(ftar_comm *c, int phase, int step, int point)
             fprintf(stderr, "ftar: rank %d dies mid-exchange (phase %d step %d): own kernel %s, %d peers launched\n",
                     c->wrank, phase, step, busy ? "in flight" : "complete", peers);
         }
+#ifdef FTAR_TEST_HOOKS
         if (getenv("FTAR_KILL_WITHDRAW")) {
-            /* TEST-ONLY: the victim's input is gone with it (as after the loss of its device):
-             * its workspace generation moves on and its published sbuf is withdrawn, so no
-             * peer may read either (ftar_dead_input) */
+            /* TEST-ONLY (the hooks build, lib/libftar_hooks.so and host-sim): the victim's
+             * input is gone with it (as after the loss of its device): its workspace
+             * generation moves on and its published sbuf is withdrawn, so no peer may read
+             * either (ftar_dead_input) */
             ftar_slot *me = &c->job.shm->slot[c->wrank];
             atomic_fetch_add(&me->ws_gen, 1);
             me->uid = 0;
             me->useq = 0;
             fprintf(stderr, "ftar: rank %d withdraws its input before dying\n", c->wrank);
         }
+#endif
         if (c->verbose) fprintf(stderr, "ftar: rank %d dies at phase %d step %d point %d\n", c->wrank, phase, step, point);
         fflush(stdout);
         fflush(stderr);
@@ -145,6 +148,7 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
 {
     *out = NULL;
     if (!job || rank < 0 || size < 1 || rank >= size || size > FTAR_MAX_RANKS) return FTAR_ERR_ARG;
+    const char *e;
     ftar_comm *c = (ftar_comm *)calloc(1, sizeof(ftar_comm));
     if (!c) return FTAR_ERR_NOMEM;
     c->wrank = rank;
@@ -154,17 +158,23 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->loop_seconds = getenv("FTAR_LOOP_SECONDS") ? atof(getenv("FTAR_LOOP_SECONDS")) : 0.0;
     c->overlap = getenv("FTAR_OVERLAP") ? atoi(getenv("FTAR_OVERLAP")) : 1;
     c->relay = getenv("FTAR_RELAY") ? atoi(getenv("FTAR_RELAY")) : 1;
-    c->redundancy = getenv("FTAR_REDUNDANCY") ? atoi(getenv("FTAR_REDUNDANCY")) : 2;
-    if (c->redundancy < 0 || c->redundancy > 2) {
-        /* the same values ftar_comm_set_option accepts (it refuses others with FTAR_ERR_ARG) */
-        fprintf(stderr, "ftar: rank %d: FTAR_REDUNDANCY=%s is not 0, 1 or 2: refused\n", rank,
-                getenv("FTAR_REDUNDANCY"));
-        free(c);
-        return FTAR_ERR_ARG;
+    c->redundancy = 2;
+    if ((e = getenv("FTAR_REDUNDANCY"))) {
+        /* the same values ftar_comm_set_option accepts (it refuses others with FTAR_ERR_ARG);
+         * the whole string must be the number: "auto", "on" or "" are refused, not read as 0 */
+        char *end = NULL;
+        long v = strtol(e, &end, 10);
+        if (end == e || *end != 0 || v < 0 || v > 2) {
+            fprintf(stderr, "ftar: rank %d: FTAR_REDUNDANCY=%s is not 0, 1 or 2: refused\n", rank, e);
+            free(c);
+            return FTAR_ERR_ARG;
+        }
+        c->redundancy = (int)v;
     }
     c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
     c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
     c->push = getenv("FTAR_PUSH") ? atoi(getenv("FTAR_PUSH")) : 0;
+    c->mesh_wait = getenv("FTAR_MESH_WAIT") ? atoi(getenv("FTAR_MESH_WAIT")) != 0 : 1;
     c->gate = getenv("FTAR_GATE") ? atoi(getenv("FTAR_GATE")) != 0 : 1;
     c->gate_hold_s = (getenv("FTAR_GATE_HOLD_US") ? atof(getenv("FTAR_GATE_HOLD_US")) : 2000.0) * 1e-6;
     c->gate_max = getenv("FTAR_GATE_MAX") ? (size_t)atoll(getenv("FTAR_GATE_MAX")) : ((size_t)1 << 20);
@@ -371,7 +381,7 @@ void ftar_resolve_inputs(ftar_comm *c)
             c->export_user = 0;
             me->uid = 0; /* this call's input is the staged IN from here on (ftar_dead_input) */
             if (c->in_alias) { /* stage the whole vector: what every schedule reads from IN */
-                fdev_seg s = {FDEV_COPY, 0, c->ws[WS_IN], c->in_alias, NULL, c->in_bytes / 4, NULL, 0};
+                fdev_seg s = {FDEV_COPY, 0, c->ws[WS_IN], c->in_alias, NULL, c->in_bytes / 4, NULL};
                 ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL);
                 ftar_drain(c);
             }
@@ -473,6 +483,7 @@ int ftar_comm_set_option(ftar_comm *c, ftar_option opt, double v)
     case FTAR_OPT_MESH: c->mesh = v != 0; break;
     case FTAR_OPT_ONESHOT_MAX: c->oneshot_max = (size_t)v; break;
     case FTAR_OPT_PUSH: c->push = v >= 2 ? 2 : v != 0; break;
+    case FTAR_OPT_MESH_WAIT: c->mesh_wait = v != 0; break;
     case FTAR_OPT_GATE: c->gate = v != 0; break;
     case FTAR_OPT_GATE_MAX: c->gate_max = (size_t)v; break;
     case FTAR_OPT_FLAG_SYNC:
@@ -499,6 +510,7 @@ int ftar_comm_get_option(const ftar_comm *c, ftar_option opt, double *v)
     case FTAR_OPT_MESH: *v = c->mesh; break;
     case FTAR_OPT_ONESHOT_MAX: *v = (double)c->oneshot_max; break;
     case FTAR_OPT_PUSH: *v = c->push; break;
+    case FTAR_OPT_MESH_WAIT: *v = c->mesh_wait; break;
     case FTAR_OPT_GATE: *v = c->gate; break;
     case FTAR_OPT_GATE_MAX: *v = (double)c->gate_max; break;
     case FTAR_OPT_FLAG_SYNC: *v = fdev_get_knob(c->dev, FDEV_KNOB_FLAG_SYNC); break;
@@ -534,7 +546,7 @@ uint64_t ftar_step_sync(ftar_comm *c, int nsteps)
         while (now_s() - t0 < d) {
             if (c->pad_src && c->pad) {
                 size_t n = c->pad_bytes < FTAR_PAD_BYTES ? c->pad_bytes : FTAR_PAD_BYTES;
-                fdev_seg s = {FDEV_COPY, FDEV_REMOTE_X, c->pad, c->pad_src, NULL, n / 4, NULL, 0};
+                fdev_seg s = {FDEV_COPY, FDEV_REMOTE_X, c->pad, c->pad_src, NULL, n / 4, NULL};
                 const void *src = c->pad_src;
                 if (n / 4 == 0 || ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL)) break;
                 ftar_drain(c);
@@ -684,8 +696,7 @@ int ftar_prelaunch(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int ns
 static int seg_eq(const fdev_seg *a, const fdev_seg *b)
 {
     return a->kind == b->kind && a->remote == b->remote && a->out == b->out && a->x == b->x &&
-           (a->kind == FDEV_COPY || a->y == b->y) && a->n == b->n && a->out2 == b->out2 &&
-           (!a->out2 || a->out2_pre == b->out2_pre);
+           (a->kind == FDEV_COPY || a->y == b->y) && a->n == b->n && a->out2 == b->out2;
 }
 
 void ftar_run_gated_or(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
@@ -704,10 +715,57 @@ void ftar_run_gated_or(ftar_comm *c, int dtype, int op, const fdev_seg *segs, in
     if (nseg) ftar_run(c, dtype, op, segs, nseg, tag);
 }
 
+/* A _host entry point's copy (H2D / D2H, or the wait for one) failed on this rank: the job
+ * ends (MPI_Abort), as the device path ends it on a launch error.  Returning FTAR_ERR_DEVICE
+ * alone would leave the peers spinning in the collective's next barrier for a rank that is
+ * alive but gone (the reference's MPI_ERRORS_ARE_FATAL outside the tolerant
+ * loops, raben/rabenseifner.c:358-360, rd/recursive_doubling.c:73-75). */
+void ftar_host_copy_failed(ftar_comm *c, const char *what)
+{
+    fprintf(stderr, "ftar: rank %d: %s failed: %s\n", c->wrank, what, fdev_last_error());
+    ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+}
+
 int ftar_drain(ftar_comm *c)
 {
     double t0 = now_s();
     int rc = fdev_sync(c->dev, ftar_ctrl_poll, &c->job);
+    if (!rc) atomic_store_explicit(&c->job.shm->slot[c->wrank].inflight, 0, memory_order_release);
+    c->stats.drain_s += now_s() - t0;
+    if (rc) {
+        fprintf(stderr, "ftar: rank %d: device error: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    return rc;
+}
+
+void *ftar_flag(ftar_comm *c, int w)
+{
+    if (w == c->wrank) return c->ws[WS_W] ? (char *)c->ws[WS_W] + c->ws_bytes - FDEV_FLAG_BYTES : NULL;
+    return c->peer[w][WS_W] ? (char *)c->peer[w][WS_W] + c->peer_bytes[w] - FDEV_FLAG_BYTES : NULL;
+}
+
+int ftar_watch_peers(void *arg)
+{
+    ftar_comm *c = (ftar_comm *)arg;
+    ftar_ctrl_poll(&c->job); /* an abort ends this process here */
+    double t = now_s();
+    if (t - c->watch_t < 50e-6) return 0;
+    c->watch_t = t;
+    for (int i = 0; i < c->size; i++) {
+        int w = c->order[i];
+        if (w != c->wrank && ftar_is_dead(c, w)) {
+            fdev_peer_wait_abort(c->dev); /* the wait returns; the next agree reports the failure */
+            break;
+        }
+    }
+    return 0;
+}
+
+int ftar_drain_watch(ftar_comm *c)
+{
+    double t0 = now_s();
+    int rc = fdev_sync(c->dev, ftar_watch_peers, c);
     if (!rc) atomic_store_explicit(&c->job.shm->slot[c->wrank].inflight, 0, memory_order_release);
     c->stats.drain_s += now_s() - t0;
     if (rc) {
@@ -783,7 +841,7 @@ int ftar_single_rank(ftar_comm *c, const void *sbuf, void *rbuf, size_t bytes)
     ftar_maybe_die(c, FTAR_PH_PRE, 0, FTAR_PT_BEFORE);
     ftar_enter(c);
     if (sbuf != rbuf) {
-        fdev_seg s = {FDEV_COPY, 0, rbuf, sbuf, NULL, bytes / 4, NULL, 0};
+        fdev_seg s = {FDEV_COPY, 0, rbuf, sbuf, NULL, bytes / 4, NULL};
         ftar_run(c, FTAR_INT32, FTAR_SUM, &s, 1, FDEV_TAG_LOCAL);
     }
     ftar_launched(c, FTAR_PH_PRE, 0);
@@ -827,6 +885,7 @@ void *ftar_local(ftar_comm *c, int b)
  * round 2).  Costs the old workspace's memory for the length of the call. */
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
 {
+    bytes += FDEV_FLAG_BYTES; /* the peer-wait flag page at the end (ftar_flag) */
     if (bytes <= c->ws_bytes && c->ws[0]) return FTAR_SUCCESS;
     if (c->ws[0] && bytes < 2 * c->ws_bytes) bytes = 2 * c->ws_bytes; /* grow geometrically: few re-exports */
     size_t nb = (bytes + WS_ALIGN - 1) / WS_ALIGN * WS_ALIGN;

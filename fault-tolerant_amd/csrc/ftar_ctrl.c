@@ -68,10 +68,13 @@ int ftar_ctrl_create(ftar_job *job, const char *name, int size)
     close(fd);
     if (rc) return rc;
     memset(job->shm, 0, sizeof(ftar_shm));
-    job->shm->magic = FTAR_SHM_MAGIC;
     job->shm->version = FTAR_SHM_VERSION;
+    job->shm->abi_id = FTAR_ABI_ID;
     job->shm->size = size;
     for (int i = 0; i < FTAR_DECISIONS; i++) atomic_store(&job->shm->decision[i], FTAR_UNDECIDED);
+    /* the magic last: a rank that reads it (ftar_ctrl_attach's header check) reads the
+     * version and build written before it */
+    __atomic_store_n(&job->shm->magic, FTAR_SHM_MAGIC, __ATOMIC_RELEASE);
     atomic_store_explicit(&job->shm->ready, 1, memory_order_release);
     job->size = size;
     job->rank = -1;
@@ -95,6 +98,22 @@ int ftar_ctrl_attach(ftar_job *job, const char *name, int rank, int size, int cr
         int fd = shm_open(name, O_RDWR, 0600);
         if (fd >= 0) {
             struct stat st;
+            /* the header (magic, version, build) is read before anything else: a launcher of
+             * other headers is refused with one clear line, whatever its block's layout */
+            struct {
+                uint32_t magic, version;
+                uint64_t abi_id;
+            } hdr;
+            if (pread(fd, &hdr, sizeof(hdr), 0) == (ssize_t)sizeof(hdr) && hdr.magic == FTAR_SHM_MAGIC &&
+                (hdr.version != FTAR_SHM_VERSION || hdr.abi_id != FTAR_ABI_ID)) {
+                fprintf(stderr, "ftar: rank %d: control block %s was created by build %016llx (layout %u), this "
+                                "library is build %016llx (layout %u): launcher and library from different "
+                                "builds -- rebuild both (make)\n",
+                        rank, name, hdr.version == FTAR_SHM_VERSION ? (unsigned long long)hdr.abi_id : 0ull,
+                        hdr.version, (unsigned long long)FTAR_ABI_ID, FTAR_SHM_VERSION);
+                close(fd);
+                return FTAR_ERR_STATE;
+            }
             if (fstat(fd, &st) == 0 && st.st_size > 0 && (size_t)st.st_size != sizeof(ftar_shm)) {
                 fprintf(stderr, "ftar: rank %d: control block %s has %lld bytes, this build expects %zu "
                                 "(launcher and library from different builds?)\n",

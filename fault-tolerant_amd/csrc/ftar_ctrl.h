@@ -25,7 +25,12 @@
 #include "ftar_dev.h"
 
 #define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
-#define FTAR_SHM_VERSION 5
+#define FTAR_SHM_VERSION 6
+/* digest of the headers this binary was built from (fault-tolerant_amd/tools/build_id.sh abi,
+ * passed by the Makefiles): the launcher writes it into the control block, every rank compares */
+#ifndef FTAR_ABI_ID
+#define FTAR_ABI_ID 0ull
+#endif
 #define FTAR_NBUF 4       /* exported workspace buffers per rank (IN, W, T, R) */
 #define FTAR_DECISIONS 64 /* ring of agree decisions */
 
@@ -81,6 +86,7 @@ typedef struct {
 typedef struct {
     uint32_t magic;
     uint32_t version;
+    uint64_t abi_id;                /* FTAR_ABI_ID of the binary that created the block */
     int size;
     _Atomic int ready;
     _Atomic uint64_t failed;        /* one bit per original rank, monotone */

@@ -39,8 +39,6 @@ typedef struct {
     const void *y;
     size_t n;         /* elements */
     void *out2;       /* optional second destination receiving the same values (local) */
-    int out2_pre;     /* FDEV_REDUCE only: out2 receives x as it was read (the pre-image of an in-place
-                         reduce), not the result */
 } fdev_seg;
 
 #define FDEV_MAX_SEGS 16 /* a relayed exchange step: 2 own pulls + 2 x 6 relay duties */
@@ -138,6 +136,25 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
  * the workgroups returned without touching memory) is caught by the next fdev_sync, which
  * relaunches the same plan ungated and drains it (fdev_gate_relaunches counts them). */
 int fdev_gate_open(ftar_dev *d, int skip);
+
+/* Device-side order between ranks (the mesh allgather behind the peers' reduce-scatter, with
+ * no host barrier between them).  fdev_peer_wait queues, on the main stream:
+ * a fenced marker (everything queued so far is released to HBM, device-wide), the store of
+ * `token` into `flag` (a word of this rank's exported HBM, FDEV_FLAG_BYTES at the end of its
+ * W), then a one-wavefront kernel that waits until every peer's flag holds `token`.  The NEXT
+ * launch on the main stream runs behind a fenced marker (the peers' data read fresh) and only
+ * if that wait succeeded: when the host gives it up (fdev_peer_wait_abort: a peer died), or it
+ * times out (FTAR_GATE_TIMEOUT_MS), its workgroups return untouched, and after the drain
+ * fdev_peer_wait_verdict returns 0.  Host-sim: the wait spins on the host, calling `poll`
+ * (which may call fdev_peer_wait_abort); the GPU build ignores poll (the drain's poll does
+ * that).  Tokens only grow: a flag holding a later token satisfies an earlier wait. */
+#define FDEV_FLAG_BYTES 4096
+#define FDEV_MAX_PEERS 15
+int fdev_peer_wait(ftar_dev *d, void *flag, void *const *peer_flags, int npeers, uint64_t token,
+                   int (*poll)(void *), void *arg);
+void fdev_peer_wait_abort(ftar_dev *d);
+/* after the drain of the launch behind the wait: 1 it ran (or none was armed), 0 it was skipped */
+int fdev_peer_wait_verdict(ftar_dev *d);
 /* 1 while a gated launch waits for its gate. */
 int fdev_gate_pending(const ftar_dev *d);
 int fdev_gate_relaunches(const ftar_dev *d);

@@ -180,6 +180,12 @@ struct ftar_dev {
     int tr_drop;       // FTAR_TRACE_DROP (test-only): 1 = marker drains without their system fence, 2 = no acquires
     hipEvent_t nofence_main, nofence_bg; // the unfenced markers of tr_drop = 1
     unsigned long long tr_n;
+    // fdev_peer_wait: the wait kernel's verdict words (sig_flag[48] pinned, gate_dw[48] device),
+    // the host's abort word (sig_flag[49]); pw_pending: the next main-stream launch runs behind
+    // the wait; pw_armed: its verdict is read after the drain
+    unsigned pw_seq, pw_vval;
+    int pw_pending, pw_armed;
+    unsigned long long pw_launch_n;
 };
 
 extern "C" {
@@ -291,6 +297,9 @@ int fdev_open(int device, ftar_dev **out)
     d->tr_fenced = d->tr_drop = 0;
     d->nofence_main = d->nofence_bg = nullptr;
     d->tr_n = 0;
+    d->pw_seq = d->pw_vval = 0;
+    d->pw_pending = d->pw_armed = 0;
+    d->pw_launch_n = 0;
     memset(d->h2d_done, 0, sizeof(d->h2d_done));
     // Peer access to every other GPU of the node: the exchanges read peers' HBM.
     for (int p = 0; p < ndev; p++) {
@@ -370,6 +379,12 @@ int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
             memcpy(handle, &h, FDEV_HANDLE_BYTES);
             *ptr = p;
             if (held) (void)hipFree(held);
+            // the last FDEV_FLAG_BYTES start zeroed: the peer-wait flag of a W buffer never
+            // holds a token before its owner publishes one (fdev_peer_wait)
+            if (bytes >= FDEV_FLAG_BYTES) {
+                HIPCHK(hipMemsetAsync((char *)p + bytes - FDEV_FLAG_BYTES, 0, FDEV_FLAG_BYTES, d->stream));
+                HIPCHK(hipStreamSynchronize(d->stream));
+            }
             return 0;
         }
         (void)hipGetLastError();
@@ -646,7 +661,6 @@ static void seg_inputs(const fdev_seg *segs, int nseg, size_t es, ftar::SegIn *i
         in[i].y = segs[i].y;
         in[i].n = segs[i].n;
         in[i].out2 = segs[i].out2;
-        in[i].out2_pre = segs[i].out2_pre;
         double b = (double)segs[i].n * (double)es;
         int nread = segs[i].kind == FDEV_COPY ? 1 : 2;
         int nremote = ((segs[i].remote & FDEV_REMOTE_X) ? 1 : 0) +
@@ -678,13 +692,28 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
     d->ctr.hbm_bytes += hbm;
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(in, nseg, es, d->max_blocks, &L);
+    const bool behind_wait = d->pw_pending && st == d->stream;
+    if (behind_wait) d->pw_pending = 0;
     if (grid == 0) return 0;
     L.nt_store = nt_store();
     note_launch(d, st, grid, true, &L.sig);
+    if (behind_wait) {
+        // behind a peer wait: a fenced marker first (device-wide acquire: the peers' data read
+        // fresh, not from lines this GPU cached before), then the wait's verdict decides
+        if (!d->tr_fenced && d->tr_drop != 2) { // tr_drop 2: TEST-ONLY, acquires left out
+            HIPCHK(hipEventRecord(d->fence_main, st));
+            d->tr_fenced = 1;
+        }
+        d->need_acquire = 0;
+        L.sig.vword = d->gate_dw + 48;
+        L.sig.vval = d->pw_vval;
+        d->pw_armed = 1;
+    }
     if (d->trace) {
         std::vector<TrRange> rd, wr;
         seg_ranges(segs, nseg, es, rd, wr);
         tr_launch(d, st, &L.sig, tr_rw(d, rd, wr), 0, "k");
+        if (behind_wait) d->pw_launch_n = d->tr_n;
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (d->profiling) {
@@ -1357,6 +1386,73 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 
 void fdev_fence_next_drain(ftar_dev *d) { d->force_fence = 1; }
 
+int fdev_peer_wait(ftar_dev *d, void *flag, void *const *peer_flags, int npeers, uint64_t token,
+                   int (*poll)(void *), void *arg)
+{
+    (void)poll;
+    (void)arg;
+    if (!d->sig_flag || !d->gate_dw || !flag || npeers < 1 || npeers > ftar::kMaxPeers) {
+        snprintf(g_err, sizeof(g_err), "fdev_peer_wait: unavailable (%s) or bad arguments",
+                 d->sig_flag ? "flag words" : "FTAR_FLAG_SYNC=0");
+        return 13;
+    }
+    if (d->gate_pending) (void)fdev_gate_open(d, 1); // nothing waits behind a closed gate
+    ftar::PeerWait W{};
+    W.own = (unsigned long long *)flag;
+    for (int i = 0; i < npeers; i++) W.peer[i] = (const unsigned long long *)peer_flags[i];
+    W.npeers = npeers;
+    W.token = (unsigned long long)token;
+    d->pw_seq++;
+    d->pw_vval = 2u * d->pw_seq;
+    __atomic_store_n(d->sig_flag + 48, 0u, __ATOMIC_RELAXED); // verdict
+    __atomic_store_n(d->sig_flag + 49, 0u, __ATOMIC_RELEASE); // abort word
+    W.abort_word = d->sig_flag + 49;
+    W.verdict_dev = d->gate_dw + 48;
+    W.verdict_host = d->sig_flag + 48;
+    W.vval = d->pw_vval;
+    W.ticks = d->gate_ticks;
+    // release: everything this rank queued so far is in HBM, device-wide, before its flag
+    if (d->tr_drop == 1) { // TEST-ONLY (FTAR_TRACE_DROP=release): the flag without the release
+        if (!d->nofence_main)
+            HIPCHK(hipEventCreateWithFlags(&d->nofence_main, hipEventDisableTiming | hipEventDisableSystemFence));
+        HIPCHK(hipEventRecord(d->nofence_main, d->stream));
+    } else {
+        HIPCHK(hipEventRecord(d->fence_main, d->stream));
+    }
+    if (d->trace) {
+        std::string own, peers;
+        tr_fmt(d, {{flag, 8}}, own);
+        std::vector<TrRange> pr;
+        for (int i = 0; i < npeers; i++) pr.push_back({peer_flags[i], 8});
+        tr_fmt(d, pr, peers);
+        if (d->tr_drop != 1) tr(d, "M pub"); // the fenced marker in front of the flag (a release, not a drain)
+        tr(d, "F %llu w=%s", (unsigned long long)token, own.c_str());
+        tr(d, "V %llu r=%s", (unsigned long long)token, peers.c_str());
+    }
+    hipError_t e = ftar::launch_peer_wait(W, d->stream);
+    if (e != hipSuccess) return set_err(e, "peer_wait_kernel launch");
+    d->unsignalled++; // drained through a fenced marker
+    d->need_acquire = 0;
+    d->pw_pending = 1;
+    d->pw_armed = 0;
+    return 0;
+}
+
+void fdev_peer_wait_abort(ftar_dev *d)
+{
+    if (d->sig_flag && d->pw_vval) __atomic_store_n(d->sig_flag + 49, d->pw_vval, __ATOMIC_RELEASE);
+}
+
+int fdev_peer_wait_verdict(ftar_dev *d)
+{
+    d->pw_pending = 0;
+    if (!d->pw_armed) return 1;
+    d->pw_armed = 0;
+    if (__atomic_load_n(d->sig_flag + 48, __ATOMIC_ACQUIRE) == d->pw_vval) return 1;
+    tr(d, "S %llu", d->pw_launch_n); // the launch behind the wait returned untouched
+    return 0;
+}
+
 int fdev_busy(ftar_dev *d)
 {
     hipError_t e = hipStreamQuery(d->stream);
@@ -1519,8 +1615,12 @@ int fdev_trace_open(ftar_dev *d, const char *path)
         return 13;
     }
     setvbuf(d->trace, nullptr, _IOLBF, 0); // a killed rank leaves every line it wrote
+#ifdef FTAR_TEST_HOOKS
+    // TEST-ONLY (lib/libftar_hooks.so): drop a release or an acquire, so that
+    // tests/test_gpu_fences.py can show the fence checker fails without it
     const char *dr = getenv("FTAR_TRACE_DROP");
     d->tr_drop = !dr ? 0 : !strcmp(dr, "release") ? 1 : !strcmp(dr, "acquire") ? 2 : 0;
+#endif
     tr(d, "# ftar trace: device %d, flag_sync %d, drop %d", d->device, d->flag_sync, d->tr_drop);
     return 0;
 }
@@ -1604,7 +1704,7 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
         return 0;
     }
     // MPI_Reduce_local(in, inout): inout = inout <op> in  -> x = inout, y = in
-    ftar::SegIn seg{ftar::kReduce, inout, inout, in, n, nullptr, 0};
+    ftar::SegIn seg{ftar::kReduce, inout, inout, in, n, nullptr};
     ftar::KSegList L;
     unsigned grid = ftar::plan_segments(&seg, 1, es, cached_blocks, &L);
     if (grid == 0) return 0;

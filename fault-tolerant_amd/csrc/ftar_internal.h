@@ -86,6 +86,8 @@ struct ftar_comm {
                             comm spans GPUs), 1 always, 0 never (a replay reads the dead rank's IN) */
     int mesh;            /* FTAR_MESH (default 1): one-hop Raben at power-of-two p without a spare */
     int push;            /* FTAR_PUSH (default 0): the mesh by remote stores -- 1 reduce-scatter, 2 both phases */
+    int mesh_wait;       /* FTAR_MESH_WAIT (default 1): the mesh's allgather ordered behind the peers' trees on the device */
+    double watch_t;      /* ftar_watch_peers: when the members were last checked for deaths */
     int gate;            /* FTAR_GATE (default 1): small exchange launches queued ahead of their barrier, gated */
     double gate_hold_s;  /* FTAR_GATE_HOLD_US: a barrier waiting longer gives the pending gated launch up (0 = never) */
     size_t gate_max;     /* FTAR_GATE_MAX bytes (default 1 MiB): largest vector whose launches are queued ahead */
@@ -115,8 +117,15 @@ int ftar_comm_rank_of(const ftar_comm *c, int w);
 
 /* collective: grow the _host entry points' staging to `bytes` (aborts the job on failure) */
 int ftar_ensure_staging(ftar_comm *c, size_t bytes);
-/* collective: grow the exported workspace to hold `bytes` per buffer */
+/* collective: grow the exported workspace to hold `bytes` per buffer (plus the peer-wait flag
+ * page, FDEV_FLAG_BYTES at the end of each buffer) */
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes);
+/* the peer-wait flag of original rank w: the last FDEV_FLAG_BYTES of its W (NULL: not mapped) */
+void *ftar_flag(ftar_comm *c, int w);
+/* fdev_sync's poll while a launch waits on the device for the peers (fdev_peer_wait): the
+ * failure detector, and a dead member gives the wait up (fdev_peer_wait_abort) */
+int ftar_watch_peers(void *arg);
+int ftar_drain_watch(ftar_comm *c);
 /* pointer to buffer b of original rank w (own or peer mapping) */
 void *ftar_buf(ftar_comm *c, int w, int b);
 /* this rank's buffer b: a workspace buffer or the call's WS_UIN / WS_UOUT */
@@ -144,6 +153,7 @@ int64_t ftar_peer_pub(ftar_comm *c, int w);
 /* agree outside the tolerant region: any new failure aborts the job */
 void ftar_sync_fatal(ftar_comm *c);
 /* drain the device stream (busy wait, abort-aware) */
+void ftar_host_copy_failed(ftar_comm *c, const char *what); /* aborts the job */
 int ftar_drain(ftar_comm *c);
 /* enqueue one segment kernel */
 int ftar_run(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int nseg, int tag);

@@ -60,7 +60,34 @@ struct KSignal {
     unsigned stage_es;
     unsigned stage_tag;
     unsigned *stage_cnt;  // device counter (agent scope)
+    // Behind a peer wait (PeerWait, queued just before on the same stream): every workgroup
+    // runs only if the wait kernel wrote `vval` into the device word *vword (go); any other
+    // value (vval | 1: given up) and it returns untouched.  nullptr = no wait in front.
+    const unsigned *vword;
+    unsigned vval;
 };
+
+// The wait of the mesh allgather for the peers' reduce-scatter (fdev_peer_wait): ONE
+// wavefront.  Lane 0 first publishes this rank's flag (`token` into *own, system scope, then
+// written back: the tree's data was released to HBM device-wide by the fenced marker in front
+// of this kernel); then lane i polls peer i's flag over xGMI (system-scope loads, uncached)
+// until every one holds at least `token`, the host's abort word holds vval (a peer died: give
+// up), or `ticks` of the wall clock pass (give up, so the grid always drains).  The verdict
+// (vval = go, vval | 1 = given up) goes to *verdict_dev for the launch behind it and to the
+// pinned host word *verdict_host for the host after its drain.
+constexpr int kMaxPeers = 15;
+struct PeerWait {
+    unsigned long long *own;
+    const unsigned long long *peer[kMaxPeers];
+    int npeers;
+    unsigned long long token;
+    const unsigned *abort_word;
+    unsigned *verdict_dev;
+    unsigned *verdict_host;
+    unsigned vval;
+    unsigned long long ticks;
+};
+hipError_t launch_peer_wait(const PeerWait &W, hipStream_t s);
 
 struct KSeg {
     void *out;
@@ -70,7 +97,6 @@ struct KSeg {
     size_t n;
     unsigned kind;
     unsigned vec;
-    unsigned pre2;       // reduce: out2 receives x as read (the pre-image), not the result
     unsigned blk_begin;  // sequential region: blocks [blk_begin, blk_end) ...
     unsigned blk_end;
     unsigned tile_base;  // ... take tiles tile_base, tile_base + 1, ... of this piece
@@ -127,7 +153,6 @@ struct SegIn {
     const void *y;
     size_t n;
     void *out2;
-    int out2_pre; // reduce: out2 receives x (pre-image)
 };
 
 // Tree reduce: out[i] = balanced left-to-right tree of src[0..p-1][i] (p = 2, 4, 8, 16):

@@ -225,6 +225,12 @@ __device__ __forceinline__ unsigned gate_wait(const KSignal &G, const unsigned *
 
 __device__ __forceinline__ bool signal_gate(const KSignal &G)
 {
+    if (G.vword) { // behind a peer wait: its verdict is in device memory already (stream order)
+        __shared__ unsigned vgo;
+        if (threadIdx.x == 0) vgo = __hip_atomic_load(G.vword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G.vval;
+        __syncthreads();
+        if (!vgo) return false;
+    }
     if (!G.gate) return true;
     __shared__ unsigned go;
     if (threadIdx.x == 0) {
@@ -278,9 +284,6 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk, u
     const uint4 *__restrict__ Y = (const uint4 *)S.y;
     uint4 *__restrict__ O = (uint4 *)S.out;
     uint4 *__restrict__ O2 = (uint4 *)S.out2; // wave-uniform: both stores or one
-    // pre2 (wave-uniform): O2 receives x as read -- the pre-image of an in-place reduce,
-    // saved by the same pass that overwrites it (the configs[4] mid-exchange guard)
-    const bool pre = S.pre2 != 0 && S.kind != kCopy;
     const size_t nv = S.n / E;
     for (size_t base = b * kTile; base < nv; base += nblk * kTile) {
         const size_t i = base + threadIdx.x;
@@ -291,16 +294,12 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk, u
             if (S.kind != kCopy) {
 #pragma unroll
                 for (int u = 0; u < kUnroll; u++) c[u] = ldnt(Y + i + u * kBlock);
-                if (pre) {
-#pragma unroll
-                    for (int u = 0; u < kUnroll; u++) st16(O2 + i + u * kBlock, a[u], nts);
-                }
 #pragma unroll
                 for (int u = 0; u < kUnroll; u++) a[u] = apply16<T, OP>(a[u], c[u]);
             }
 #pragma unroll
             for (int u = 0; u < kUnroll; u++) st16(O + i + u * kBlock, a[u], nts);
-            if (O2 && !pre) {
+            if (O2) {
 #pragma unroll
                 for (int u = 0; u < kUnroll; u++) st16(O2 + i + u * kBlock, a[u], nts);
             }
@@ -309,7 +308,7 @@ __device__ __forceinline__ void vec_body(const KSeg &S, size_t b, size_t nblk, u
                 const uint4 xv = ldnt(X + j);
                 const uint4 v = (S.kind == kCopy) ? xv : apply16<T, OP>(xv, ldnt(Y + j));
                 st16(O + j, v, nts);
-                if (O2) st16(O2 + j, pre ? xv : v, nts);
+                if (O2) st16(O2 + j, v, nts);
             }
         }
     }
@@ -322,13 +321,12 @@ __device__ __forceinline__ void scalar_body(const KSeg &S, size_t b, size_t nblk
     const T *Y = (const T *)S.y;
     T *O = (T *)S.out;
     T *O2 = (T *)S.out2;
-    const bool pre = S.pre2 != 0 && S.kind != kCopy;
     const size_t stride = nblk * kBlock;
     for (size_t i = b * kBlock + threadIdx.x; i < S.n; i += stride) {
         const T xv = X[i];
         const T v = (S.kind == kCopy) ? xv : apply<T, OP>(xv, Y[i]);
         O[i] = v;
-        if (O2) O2[i] = pre ? xv : v;
+        if (O2) O2[i] = v;
     }
 }
 
@@ -626,6 +624,45 @@ static hipError_t launch_t(int op, const KSegList &L, unsigned grid, hipStream_t
     });
 }
 
+// PeerWait (ftar_kernels.h): one wavefront, lane i < npeers polls peer i's flag.
+__global__ __launch_bounds__(64) void peer_wait_kernel(PeerWait W)
+{
+    const int lane = threadIdx.x;
+    if (lane == 0) {
+        __hip_atomic_store(W.own, W.token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // system scope: the flag's line to HBM for the peers
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned long long *mine = lane < W.npeers ? W.peer[lane] : nullptr;
+    const unsigned long long t0 = wall_clock64();
+    bool go = false;
+    for (;;) {
+        const bool ready = !mine || __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= W.token;
+        if (__all(ready)) {
+            go = true;
+            break;
+        }
+        if (__hip_atomic_load(W.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == W.vval) break;
+        if (wall_clock64() - t0 > W.ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) {
+        const unsigned v = go ? W.vval : (W.vval | 1u);
+        __hip_atomic_store(W.verdict_dev, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(W.verdict_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+hipError_t launch_peer_wait(const PeerWait &W, hipStream_t s)
+{
+    if (W.npeers < 1 || W.npeers > kMaxPeers || !W.own || !W.abort_word || !W.verdict_dev || !W.verdict_host)
+        return hipErrorInvalidValue;
+    for (int i = 0; i < W.npeers; i++)
+        if (!W.peer[i]) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(peer_wait_kernel, dim3(1), dim3(64), 0, s, W);
+    return hipGetLastError();
+}
+
 hipError_t launch_segments(int dtype, int op, const KSegList &L, unsigned grid, hipStream_t s)
 {
     switch (dtype) {
@@ -699,7 +736,6 @@ unsigned plan_segments(const SegIn *in, int nin, size_t esize, unsigned max_bloc
             k.n = n;
             k.kind = (unsigned)g.kind;
             k.vec = vec;
-            k.pre2 = (g.out2 && g.out2_pre && g.kind != kCopy) ? 1u : 0u;
             k.blk_begin = k.blk_end = 0;
             pieces[np].k = k;
             pieces[np].bytes = n * esize;

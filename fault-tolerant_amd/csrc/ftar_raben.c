@@ -32,7 +32,9 @@
 #include "ftar_internal.h"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #define MAXSTEPS 32
 /* host-buffer pipeline: vectors of at least HOST_PIPE_MIN bytes go through in chunks of
@@ -57,6 +59,8 @@ typedef struct {
     int64_t slot;   /* push: elements per source slot in an owner's R */
     int oneshot;    /* mesh of a small vector: every block in its owner's tree, one launch */
     int own_in_rbuf; /* the mesh's tree stored this rank's final block in rbuf too: the allgather skips it */
+    int io_safe;     /* sbuf == rbuf or the two do not overlap: rbuf may be written while peers read sbuf */
+    int devwait;     /* the mesh's allgather ordered behind the peers' trees on the device (rb_mesh_devwait) */
     /* the one-shot launch queued ahead of the barrier (rb_oneshot_prelaunch): its plan, to
      * be checked against the one the inputs' resolution gives */
     int gated;
@@ -161,13 +165,13 @@ static void rb_plan(const rb_ctx *x, int step, int mask, int ag, ftar_plan *P)
 
 static void run_reduce(rb_ctx *x, void *out, const void *xin, const void *yin, int64_t n, int remote, int tag)
 {
-    fdev_seg s = {FDEV_REDUCE, remote, out, xin, yin, (size_t)n, NULL, 0};
+    fdev_seg s = {FDEV_REDUCE, remote, out, xin, yin, (size_t)n, NULL};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
 static void run_copy(rb_ctx *x, void *out, const void *src, int64_t n, int remote, int tag)
 {
-    fdev_seg s = {FDEV_COPY, remote, out, src, NULL, (size_t)n, NULL, 0};
+    fdev_seg s = {FDEV_COPY, remote, out, src, NULL, (size_t)n, NULL};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
@@ -255,7 +259,7 @@ static void rb_handler_rs(rb_ctx *x, uint64_t newf, int fs)
                 int64_t off = s < fs ? dsi[s + 1] : dri[fs], n = s < fs ? dsc[s + 1] : drc[fs];
                 if (n <= 0) continue;
                 seg[nseg++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, ftar_local(c, rb_acc(x, s)), off),
-                                         at(x, OW, off), NULL, (size_t)n, NULL, 0};
+                                         at(x, OW, off), NULL, (size_t)n, NULL};
             }
             if (nseg) ftar_run(c, x->dtype, x->op, seg, nseg, FDEV_TAG_RECOV);
             x->has_recov = 0;
@@ -366,7 +370,7 @@ static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf, void *rbuf)
         rb_windows(u, x->count, L, ri, si, rc, sc);
         void *R = ftar_buf(c, c->order[rb_real(x, u)], WS_R);
         segs[ns++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_OUT, rb_push_at(x, R, j, ri[L - 1]),
-                                at(x, (void *)sbuf, ri[L - 1]), NULL, (size_t)rc[L - 1], NULL, 0};
+                                at(x, (void *)sbuf, ri[L - 1]), NULL, (size_t)rc[L - 1], NULL};
     }
     double lb0 = ftar_link_bytes(c);
     ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP0);
@@ -396,7 +400,7 @@ static void rb_mesh_push_rs(rb_ctx *x, const void *sbuf, void *rbuf)
     void *out = x->push == 2 ? at(x, rbuf, own0) : at(x, W, own0);
     if (x->push == 1) { /* as the pull form: the block into rbuf too, where co-aligned (rb_mesh) */
         more[0] = at(x, rbuf, own0);
-        x->own_in_rbuf = (((uintptr_t)more[0] ^ (uintptr_t)out) & 15) == 0;
+        x->own_in_rbuf = x->io_safe && (((uintptr_t)more[0] ^ (uintptr_t)out) & 15) == 0;
         nmore = x->own_in_rbuf;
     }
     if (fdev_tree_out(c->dev, x->dtype, x->op, src, p, 0, out, more, nmore, x->push == 2, (size_t)own_n,
@@ -437,7 +441,7 @@ static int rb_mesh_push_finish(rb_ctx *x, void *rbuf)
         int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
         rb_windows(v ^ j, x->count, L, ri, si, rc, sc);
         segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, ri[L - 1]), at(x, c->ws[WS_W], ri[L - 1]), NULL,
-                                (size_t)rc[L - 1], NULL, 0};
+                                (size_t)rc[L - 1], NULL};
     }
     ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_LOCAL);
     ftar_drain(c);
@@ -479,16 +483,97 @@ static int rb_mesh_ag_segs(rb_ctx *x, void *rbuf, fdev_seg *segs)
     int ns = 0;
     if (!x->own_in_rbuf)
         segs[ns++] = (fdev_seg){FDEV_COPY, 0, at(x, rbuf, x->rindex[L - 1]), at(x, c->ws[WS_W], x->rindex[L - 1]),
-                                NULL, (size_t)x->rcount[L - 1], NULL, 0};
+                                NULL, (size_t)x->rcount[L - 1], NULL};
     for (int j = 1; j < p; j++) {
         int u = v ^ j;
         int64_t ri[MAXSTEPS], si[MAXSTEPS], rc[MAXSTEPS], sc[MAXSTEPS];
         rb_windows(u, x->count, L, ri, si, rc, sc);
         void *PW = ftar_buf(c, c->order[rb_real(x, u)], WS_W);
         segs[ns++] = (fdev_seg){FDEV_COPY, FDEV_REMOTE_X, at(x, rbuf, ri[L - 1]), at(x, PW, ri[L - 1]), NULL,
-                                (size_t)rc[L - 1], NULL, 0};
+                                (size_t)rc[L - 1], NULL};
     }
     return ns;
+}
+
+/* The mesh with its allgather ordered on the device (FTAR_OPT_MESH_WAIT), continuing
+ * rb_mesh after the tree launch.  The reduce-scatter's agree only ever served to say "every
+ * owner's block is final" -- with no idle rank every failure aborts the job at whichever
+ * agree sees it (new_entry = -1, raben/errhandler.c:207-211, 377-378) -- so that fact moves
+ * to the device: each rank releases its tree (a fenced marker) and publishes the call's token
+ * in a flag of its own HBM; the allgather, queued right behind, runs once every peer's flag
+ * holds the token.  Per call this saves one host agree round, one drain and the allgather's
+ * launch latency; the call keeps its first and last agree.  A peer that dies before
+ * publishing: the drain's failure detector gives the wait up (the allgather returns
+ * untouched), and the last agree sees the death -- the handler aborts, as at the agree this
+ * form leaves out.  A wait the device gave up with every member alive (its timeout): each
+ * rank publishes its verdict in the last agree round, so all of them learn it alike; by then
+ * every tree is released (each rank drained its own before arriving), the ranks whose
+ * allgather returned untouched launch it again (it never writes what it reads), and one more
+ * round keeps the peers' next call off their W until it is done.  Every step's kill points are passed, in the order both
+ * launches are queued: RS BEFORE, DURING; AG BEFORE, DURING; then, once drained, RS AFTER /
+ * BARRIER and AG AFTER / BARRIER. */
+static int rb_mesh_devwait(rb_ctx *x, void *rbuf, double lb0)
+{
+    ftar_comm *c = x->c;
+    const int L = x->steps, p = x->adjsize, v = x->vrank;
+    fdev_seg segs[FDEV_MAX_SEGS];
+    ftar_launched(c, FTAR_PH_LOOP, 0);
+    for (int s = 1; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_DURING);
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
+    /* the call's token: the agree sequence number, uniform over the members and only growing */
+    const uint64_t token = c->job.seq;
+#ifdef FTAR_TEST_HOOKS
+    /* TEST-ONLY: this rank's flag published late (its peers' waits time out) */
+    if (getenv("FTAR_PEER_WAIT_DELAY_US")) {
+        ftar_drain(c); /* the tree done first: the delay is in the host, not on the device */
+        usleep((useconds_t)atoll(getenv("FTAR_PEER_WAIT_DELAY_US")));
+    }
+#endif
+    void *pf[FDEV_MAX_PEERS];
+    int np = 0;
+    for (int j = 1; j < p; j++) pf[np++] = ftar_flag(c, c->order[rb_real(x, v ^ j)]);
+    if (fdev_peer_wait(c->dev, ftar_flag(c, c->wrank), pf, np, token, ftar_watch_peers, c)) {
+        fprintf(stderr, "ftar: rank %d: peer wait failed: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
+    }
+    int ns = rb_mesh_ag_segs(x, rbuf, segs);
+    ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
+    ftar_launched(c, FTAR_PH_AG, L - 1);
+    for (int s = L - 2; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_DURING);
+    ftar_drain_watch(c);
+    const int ran = fdev_peer_wait_verdict(c->dev);
+    if (!ran) c->stats.peer_wait_skips++;
+    ftar_exchange_done(c);
+    c->stats.step0_link_bytes += ftar_link_bytes(c) - lb0;
+    c->stats.steps += 2 * L;
+    c->stats.mesh_steps += 2;
+    c->stats.peer_waits++;
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_AFTER);
+    for (int s = 0; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_BARRIER);
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_AFTER);
+    for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BARRIER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BEFORE);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_DURING);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_AFTER);
+    ftar_maybe_die(c, FTAR_PH_POST, 0, FTAR_PT_BARRIER);
+    /* the reduce-scatter's and the allgather's agree and the ERRORS_ARE_FATAL barrier: one
+     * round, which also carries every rank's verdict */
+    c->pubval = ran ? 0 : 1;
+    uint64_t newf = ftar_step_sync(c, 1);
+    c->pubval = 0;
+    if (newf) rb_handler_ag(x, newf, 0); /* no idle rank: aborts */
+    int any_skipped = 0;
+    for (int i = 0; i < c->size; i++) any_skipped |= ftar_peer_pub(c, c->order[i]) != 0;
+    if (any_skipped) {
+        if (!ran) {
+            ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
+            ftar_drain(c);
+        }
+        newf = ftar_step_sync(c, 1);
+        if (newf) rb_handler_ag(x, newf, 0);
+    }
+    ftar_stats_end(c);
+    return FTAR_SUCCESS;
 }
 
 static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
@@ -527,12 +612,13 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
     /* only where rbuf is co-aligned with W (a 16-byte vector body needs every operand at the
      * same offset mod 16; otherwise the tree would fall back to scalar accesses): else the
      * allgather copies the block out of W as before */
-    x->own_in_rbuf = (((uintptr_t)own_out ^ (uintptr_t)at(x, W, own0)) & 15) == 0;
+    x->own_in_rbuf = x->io_safe && (((uintptr_t)own_out ^ (uintptr_t)at(x, W, own0)) & 15) == 0;
     if (fdev_tree_out(c->dev, x->dtype, x->op, src, p, remote, at(x, W, own0), &own_out, x->own_in_rbuf, 0,
                       (size_t)own_n, FDEV_TAG_STEP0)) {
         fprintf(stderr, "ftar: rank %d: launch failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
+    if (x->devwait) return rb_mesh_devwait(x, rbuf, lb0);
     /* up to FTAR_GATE_MAX: the allgather's launch queued right behind the tree, its gate
      * opened where it would otherwise be launched (after the reduce-scatter's agree) */
     ns = rb_mesh_ag_segs(x, rbuf, segs);
@@ -749,6 +835,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                  (c->size == 2 || count * (size_t)x->es <= c->oneshot_max);
     /* push 2 (both phases) needs every peer as an extra destination of one tree: p <= 8 */
     x->push = (x->mesh && !x->oneshot && c->push) ? (c->push == 2 && c->size <= 8 ? 2 : 1) : 0;
+    /* uniform too; every block non-empty (count >= p: the allgather launch always exists) */
+    x->devwait = x->mesh && !x->oneshot && !x->push && c->mesh_wait && count >= (size_t)c->size &&
+                 c->size - 1 <= FDEV_MAX_PEERS;
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);
@@ -771,6 +860,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * rbuf, so there sbuf and rbuf must not overlap. */
     const char *s0 = (const char *)sbuf, *d0 = (const char *)rbuf;
     int disjoint = s0 + bytes <= d0 || d0 + bytes <= s0;
+    /* partly overlapping sbuf / rbuf (neither the same buffer nor disjoint): rbuf is written
+     * only after every peer is done reading sbuf */
+    x->io_safe = disjoint || s0 == d0;
     /* The one-shot launch writes rbuf while peers still read this rank's input: in place,
      * that input must be staged (whole: peers read every block of it). */
     /* push: no peer ever reads this rank's input (it stores its parts into the owners) */
@@ -798,9 +890,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
     } else if (x->mesh) { /* peers pull every block of sbuf but this rank's own final one */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
         int64_t b0 = x->rindex[x->steps - 1], b1 = b0 + x->rcount[x->steps - 1];
-        fdev_seg cp[2] = {{FDEV_COPY, 0, IN, sbuf, NULL, (size_t)b0, NULL, 0},
+        fdev_seg cp[2] = {{FDEV_COPY, 0, IN, sbuf, NULL, (size_t)b0, NULL},
                           {FDEV_COPY, 0, at(x, IN, b1), at(x, (void *)sbuf, b1), NULL, (size_t)((int64_t)count - b1),
-                           NULL, 0}};
+                           NULL}};
         ftar_run(c, x->dtype, x->op, cp, 2, FDEV_TAG_LOCAL);
     } else if (x->fast_io) { /* the half of sbuf peers pull at step 0 */
         rb_windows(x->vrank, count, x->steps, x->rindex, x->sindex, x->rcount, x->scount);
@@ -895,9 +987,9 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                 void *PIN = ftar_buf(c, pl[0].src, WS_IN);
                 fdev_seg red = {FDEV_REDUCE, FDEV_REMOTE_Y, at(x, ftar_local(c, pl[0].dst_buf), pl[0].off),
                                 at(x, ftar_local(c, pl[0].x_buf), pl[0].off), at(x, PIN, pl[0].off), (size_t)pl[0].n,
-                                NULL, 0};
+                                NULL};
                 fdev_seg cpy = {FDEV_COPY, FDEV_REMOTE_X, at(x, T, pl[1].off), at(x, PIN, pl[1].off), NULL,
-                                (size_t)pl[1].n, NULL, 0};
+                                (size_t)pl[1].n, NULL};
                 ftar_run_pulls(c, x->dtype, x->op, &red, 1, FDEV_TAG_STEP0, 0);
                 if (x->keep_recov) {
                     ftar_run_pulls(c, x->dtype, x->op, &cpy, 1, FDEV_TAG_BG, 1);
@@ -941,7 +1033,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
             c->stats.steps++;
         }
         /* last step: this rank's own final half W -> rbuf rides in the same launch */
-        fdev_seg own = {FDEV_COPY, 0, NULL, NULL, NULL, 0, NULL, 0};
+        fdev_seg own = {FDEV_COPY, 0, NULL, NULL, NULL, 0, NULL};
         int nown = 0;
         if (step == 0 && x->vrank != -1) {
             own.out = at(x, rbuf, x->rindex[0]);
@@ -1018,10 +1110,10 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
         return ftar_allreduce_rabenseifner(sbuf, rbuf, count, dtype, op, c);
     ftar_ensure_staging(c, bytes);
     if (nchunk <= 1) {
-        if (bytes && fdev_h2d(c->dev, c->hsend, sbuf, bytes)) return FTAR_ERR_DEVICE;
+        if (bytes && fdev_h2d(c->dev, c->hsend, sbuf, bytes)) ftar_host_copy_failed(c, "H2D copy");
         int rc = ftar_allreduce_rabenseifner(c->hsend, c->hrecv, count, dtype, op, c);
         if (rc) return rc;
-        if (bytes && fdev_d2h(c->dev, rbuf, c->hrecv, bytes)) return FTAR_ERR_DEVICE;
+        if (bytes && fdev_d2h(c->dev, rbuf, c->hrecv, bytes)) ftar_host_copy_failed(c, "D2H copy");
         return FTAR_SUCCESS;
     }
     size_t per = (count + (size_t)nchunk - 1) / (size_t)nchunk;
@@ -1030,20 +1122,20 @@ int ftar_allreduce_rabenseifner_host(const void *sbuf, void *rbuf, size_t count,
     for (size_t off = 0; off < count; off += per, n++) {
         size_t m = count - off < per ? count - off : per;
         if (fdev_h2d_async(c->dev, (char *)c->hsend + off * es, (const char *)sbuf + off * es, m * es, n))
-            return FTAR_ERR_DEVICE;
+            ftar_host_copy_failed(c, "H2D copy");
     }
     n = 0;
     for (size_t off = 0; off < count; off += per, n++) {
         size_t m = count - off < per ? count - off : per;
-        if (fdev_wait_h2d(c->dev, n, ftar_ctrl_poll, &c->job)) return FTAR_ERR_DEVICE;
+        if (fdev_wait_h2d(c->dev, n, ftar_ctrl_poll, &c->job)) ftar_host_copy_failed(c, "H2D copy");
         c->chunk_cont = n > 0;
         int rc = ftar_allreduce_rabenseifner((char *)c->hsend + off * es, (char *)c->hrecv + off * es, m, dtype, op,
                                              c);
         c->chunk_cont = 0;
         if (rc) return rc;
         if (fdev_d2h_async(c->dev, (char *)rbuf + off * es, (char *)c->hrecv + off * es, m * es))
-            return FTAR_ERR_DEVICE;
+            ftar_host_copy_failed(c, "D2H copy");
     }
-    if (fdev_sync_d2h(c->dev, ftar_ctrl_poll, &c->job)) return FTAR_ERR_DEVICE;
+    if (fdev_sync_d2h(c->dev, ftar_ctrl_poll, &c->job)) ftar_host_copy_failed(c, "D2H copy");
     return FTAR_SUCCESS;
 }

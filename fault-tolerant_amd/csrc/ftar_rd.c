@@ -56,7 +56,7 @@ static int peer_cur(rd_ctx *x, int w) { return (int)ftar_peer_pub(x->c, w); }
 
 static void run1(rd_ctx *x, int kind, void *out, const void *a, const void *b, int remote, int tag)
 {
-    fdev_seg s = {kind, remote, out, a, b, x->count, NULL, 0};
+    fdev_seg s = {kind, remote, out, a, b, x->count, NULL};
     ftar_run(x->c, x->dtype, x->op, &s, 1, tag);
 }
 
@@ -365,9 +365,9 @@ int ftar_recursive_doubling_host(const void *src, void *dst, size_t count, ftar_
      * PCIe (the last step's result goes straight to dst), no staging copies */
     if (fdev_host_pinned(src) && fdev_host_pinned(dst)) return ftar_recursive_doubling(src, dst, count, dtype, op, c);
     ftar_ensure_staging(c, bytes);
-    if (bytes && fdev_h2d(c->dev, c->hsend, src, bytes)) return FTAR_ERR_DEVICE;
+    if (bytes && fdev_h2d(c->dev, c->hsend, src, bytes)) ftar_host_copy_failed(c, "H2D copy");
     int rc = ftar_recursive_doubling(c->hsend, c->hrecv, count, dtype, op, c);
     if (rc) return rc;
-    if (bytes && fdev_d2h(c->dev, dst, c->hrecv, bytes)) return FTAR_ERR_DEVICE;
+    if (bytes && fdev_d2h(c->dev, dst, c->hrecv, bytes)) ftar_host_copy_failed(c, "D2H copy");
     return FTAR_SUCCESS;
 }

@@ -173,7 +173,7 @@ void ftar_run_pulls(ftar_comm *c, int dtype, int op, const fdev_seg *segs, int n
             ftar_note_launch(c, t.x, t.n * es);
             rc = fdev_copy(c->dev, bg, t.out, t.x, t.n * es, 1, tag);
             if (t.out2) /* the second destination from the landed copy (same stream) */
-                local[nl++] = (fdev_seg){FDEV_COPY, 0, t.out2, t.out, NULL, t.n, NULL, 0};
+                local[nl++] = (fdev_seg){FDEV_COPY, 0, t.out2, t.out, NULL, t.n, NULL};
         } else {
             void *stage = staging_of(c, t.out);
             if (!stage) {

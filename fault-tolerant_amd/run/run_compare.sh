@@ -6,6 +6,7 @@
 #   ./run_compare.sh [REPEATS]        (reference: 50 repeats, NP 4..64, 1..2^27 ints)
 # One rank per GPU (RCCL refuses two ranks on one GPU), so NP defaults to 2 4 8.
 #   FTAR_CMP_NPS="2 4 8"  FTAR_CMP_BUF_MIN=1  FTAR_CMP_BUF_MAX=134217728  FTAR_TIMEOUT=60
+#   FTAR_CMP_BUF_MUL=2 (the size grid's factor: the reference doubles)
 #   FTAR_CMP_RD / FTAR_CMP_RABEN / FTAR_CMP_ORIG_RD / FTAR_CMP_ORIG_RABEN: executables
 set -u
 cd "$(dirname "$0")"
@@ -16,6 +17,7 @@ REPEATS=${1:-50}
 NPS=${FTAR_CMP_NPS:-"2 4 8"}
 BUF_MIN=${FTAR_CMP_BUF_MIN:-1}
 BUF_MAX=${FTAR_CMP_BUF_MAX:-134217728}
+BUF_MUL=${FTAR_CMP_BUF_MUL:-2}
 TIMEOUT=${FTAR_TIMEOUT:-60}
 RD=${FTAR_CMP_RD:-../src/rd/main}
 RABEN=${FTAR_CMP_RABEN:-../src/raben/main}
@@ -36,7 +38,7 @@ for rep in $(seq 1 "$REPEATS"); do
             run_one "$np" "$buf" "$ORIG_RABEN" original_raben
             run_one "$np" "$buf" "$RABEN" raben
             python3 ../analysis/check_compare.py
-            buf=$((buf * 2))
+            buf=$((buf * BUF_MUL))
         done
     done
 done

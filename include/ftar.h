@@ -222,11 +222,15 @@ typedef enum {
     FTAR_OPT_TREE_UNROLL = 11, /* 16-byte vectors per lane and source in the mesh's tree kernel at
                                   p = 4, 8 (1, 2 or 4; default 1): more loads in flight per lane for
                                   remote (xGMI) sources; same bits */
-    FTAR_OPT_GATE_MAX = 12     /* largest vector, in bytes, whose predictable launches are queued ahead
+    FTAR_OPT_GATE_MAX = 12,    /* largest vector, in bytes, whose predictable launches are queued ahead
                                   behind gates (default 1 MiB).  Above 1 MiB (mid-size: RD steps 1..,
                                   the mesh's allgather) the gate is relayed through device memory and
                                   the launch waits on up to half the CUs -- slower on a GPU shared by
                                   several ranks, so bench.py times it on the node */
+    FTAR_OPT_MESH_WAIT = 13    /* the mesh's allgather queued right behind its reduce-scatter, ordered on
+                                  the device: each rank publishes a flag in its HBM once its tree is
+                                  released, and the allgather waits for the peers' flags instead of a
+                                  host agree round and a drain (0/1, default 1) */
 } ftar_option;
 
 int ftar_comm_set_option(ftar_comm *comm, ftar_option opt, double value);
@@ -260,6 +264,8 @@ typedef struct {
     int    gate_holds;       /* gated launches given up because their barrier waited past FTAR_GATE_HOLD_US */
     int    gate_relaunches;  /* gated launches the device gave up on (gate timeout), relaunched ungated;
                                 cumulative since ftar_init */
+    int    peer_waits;       /* mesh allgathers ordered behind the peers' trees on the device (FTAR_OPT_MESH_WAIT) */
+    int    peer_wait_skips;  /* ... of them given up (a peer died, or the wait timed out) and settled by an agree */
 } ftar_stats;
 
 int ftar_last_stats(const ftar_comm *comm, ftar_stats *out);
@@ -268,6 +274,10 @@ int ftar_set_profiling(ftar_comm *comm, int on);
 
 /* Version string of the library build. */
 const char *ftar_version(void);
+/* Identity of this build: "ftar-build abi=<16 hex> src=<16 hex>" -- the digest of the
+ * headers every binary of a job shares (a launcher of other headers is refused when a rank
+ * attaches) and of every product source the library was linked from. */
+const char *ftar_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,48 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
+def pytest_sessionstart(session):
+    # host-sim segments a killed or timed-out earlier run left in /dev/shm (their owner pids
+    # are dead): removed before the suite, so it does not start short of memory
+    import harness
+    harness.reap_shm()
+
+
+def library_build_id(path=None):
+    """The 'ftar-build abi=... src=...' string baked into a built libftar.so (read from the file:
+    loading the library is not needed)."""
+    import re
+    path = path or os.path.join(ROOT, "fault-tolerant_amd", "lib", "libftar.so")
+    m = re.search(rb"ftar-build abi=[0-9a-f]{16} src=[0-9a-f]{16}", open(path, "rb").read())
+    return m.group(0).decode() if m else None
+
+
+def tree_src_id():
+    return subprocess.run([os.path.join(ROOT, "fault-tolerant_amd", "tools", "build_id.sh"), "src"],
+                          capture_output=True, text=True, check=True).stdout.strip()
+
+
+def pytest_collection_finish(session):
+    # A GPU session runs the libraries built in this tree before it was pushed: a library
+    # linked from other sources than the tree's (a stale build) would make every result
+    # evidence about some other code -- refuse to start instead (VERDICT r05 next #3)
+    if not any(it.get_closest_marker("gpu") for it in session.items):
+        return
+    try:
+        got, want = library_build_id(), tree_src_id()
+    except OSError as e:
+        pytest.exit(f"GPU session: cannot read lib/libftar.so's build id ({e}); build first (make)", returncode=3)
+    if not got or not got.endswith("src=" + want):
+        pytest.exit(f"GPU session: lib/libftar.so is '{got}' but the tree's sources are src={want}: "
+                    "stale build, rebuild (python -c 'import __graft_entry__ as g; g.build()')", returncode=3)
+    print(f"\nGPU session: {got} (the tree's sources)")
+
+
+def pytest_sessionfinish(session, exitstatus):
+    import harness
+    harness.reap_shm()
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: longer multi-process runs")

@@ -20,6 +20,13 @@ from ftar_sync) and this module verifies two rules over all ranks' logs:
   (`acq=1`: signal_acquire) or comes after a fenced marker (`fence=1`, or a `D mk` / `M pre`
   since which this rank has not read that range before barrier k -- lines cached by such a
   read could be stale).  Copy-engine reads (`eng=sdma`) do not go through the L2.
+* device order (the mesh's allgather behind the peers' trees, fdev_peer_wait) -- a read that
+  runs behind a wait `V t` for rank X's flag (queued after it, in the same round) sees X's
+  writes made before X published `F t` only if each was released by a fenced marker queued
+  between it and the flag (`M pub`), and none X made after the flag and before its next
+  arrival; `S n`: launch n returned untouched (its wait was given up).
+* no race -- without such a wait, a read in round k + 1 (after barrier k) overlaps no write X
+  made in the same round (after arriving at k, before arriving at k + 1).
 
 Reference: what each exchange must deliver, /root/reference/src/raben/rabenseifner.c:209-222
 (MPI_Sendrecv of the partner's final window of the previous step).
@@ -73,6 +80,9 @@ class RankLog:
     drains: list = field(default_factory=list)   # (line index, kind, arg)
     markers: list = field(default_factory=list)  # line indices of fenced markers (M pre)
     external: list = field(default_factory=list)  # (line index, [Access])
+    pubmarks: list = field(default_factory=list)  # line indices of the fenced markers in front of a flag (M pub)
+    pubs: dict = field(default_factory=dict)      # token -> line index of the flag's publication (F)
+    waits: list = field(default_factory=list)     # (line index, token, {owner ranks}) of device waits (V)
     drop: int = 0
 
 
@@ -123,6 +133,17 @@ def parse(path: str, rank: int) -> RankLog:
             log.drains.append((i, t[1], t[2] if len(t) > 2 else ""))
         elif k == "M":
             log.markers.append(i)
+            if len(t) > 1 and t[1] == "pub":
+                log.pubmarks.append(i)
+        elif k == "F":
+            log.pubs.setdefault(int(t[1]), i)
+        elif k == "V":
+            kv = dict(_KV.findall(line))
+            log.waits.append((i, int(t[1]), {a.owner for a in _accesses(kv.get("r", "-"))}))
+        elif k == "S":
+            for L in log.launches:
+                if L.n == int(t[1]):
+                    L.exec_idx = None
         elif k == "X":
             log.external.append((i, _accesses(t[1])))
         elif k == "A":
@@ -196,19 +217,19 @@ class Report:
 def check(logs: dict, max_report: int = 20) -> Report:
     rep = Report()
     # every write any rank made, with where it ran and where it was released
-    writes = []  # (rank, exec idx, rel idx, Access, what)
+    writes = []  # (rank, exec idx, rel idx, Access, what, stream)
     for r, log in logs.items():
         for L in log.launches:
             if L.exec_idx is not None:
                 for a in L.writes:
-                    writes.append((r, L.exec_idx, L.rel_idx, a, f"launch {L.n}"))
+                    writes.append((r, L.exec_idx, L.rel_idx, a, f"launch {L.n}", L.stream))
             for a in L.staged:
-                writes.append((r, L.idx, L.stage_rel_idx, a, f"staging of launch {L.n}"))
+                writes.append((r, L.idx, L.stage_rel_idx, a, f"staging of launch {L.n}", L.stream))
         for (i, accs) in log.external:
             rel = next((j for (j, kind, arg) in log.drains if j > i and (
                 kind == "mk" and arg == "m" or kind == "pre" and any(i < m <= j for m in log.markers))), float("inf"))
             for a in accs:
-                writes.append((r, i, rel, a, "caller's write"))
+                writes.append((r, i, rel, a, "caller's write", "x"))
     rep.writes_checked = len(writes)
     for y, log in logs.items():
         for L in log.launches:
@@ -223,8 +244,33 @@ def check(logs: dict, max_report: int = 20) -> Report:
                 if rb is None:
                     continue
                 p_idx, k = rb
+                # the device waits this launch is queued behind (same round): writer -> flag token
+                behind = {}
+                for (vi, tok, owners) in log.waits:
+                    if p_idx < vi < L.idx:
+                        for o in owners:
+                            behind[o] = tok
                 # release: every foreign write before the writer's arrival at k, released before it
-                for (x, e, rel, wa, what) in foreign:
+                for (x, e, rel, wa, what, st) in foreign:
+                    ax_k, ax_next = logs[x].arrive.get(k), logs[x].arrive.get(k + 1, float("inf"))
+                    if ax_k is not None and ax_k < e < ax_next:  # written in the reader's round
+                        if x in behind:
+                            f = logs[x].pubs.get(behind[x])
+                            if f is None:
+                                msg = f"waits for rank {x}'s flag {behind[x]}, which rank {x} never published"
+                            elif e > f:
+                                msg = f"rank {x}'s {what} (line {e}) wrote it after publishing flag {behind[x]}"
+                            elif not (rel < f or (st == "m" and any(e < m < f for m in logs[x].pubmarks))):
+                                msg = (f"rank {x}'s {what} (line {e}) wrote it and no fenced marker released it "
+                                       f"before flag {behind[x]} (line {f})")
+                            else:
+                                msg = None
+                        else:
+                            msg = f"rank {x}'s {what} (line {e}) wrote it in the same round, with no wait in between"
+                        if msg and len(rep.release) < max_report:
+                            rep.release.append(f"rank {y} launch {L.n} reads {a.owner}:{a.name}[{a.off}:+{a.n}] "
+                                               f"after barrier {k}: {msg}")
+                        continue
                     ax = logs[x].arrive.get(k)
                     if ax is None:
                         # X died before barrier k (a recovery reads its memory, or its partner

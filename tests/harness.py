@@ -35,6 +35,30 @@ class ProbeRun:
         return "MPI_ABORT" in self.stderr
 
 
+def reap_shm(prefix: str = "ftarhs-") -> int:
+    """Remove host-sim segments (/dev/shm/ftarhs-<tag>-<pid>-<seq>) whose owner process is
+    gone -- what a killed or timed-out job leaves behind; segments of live processes (another
+    pytest-xdist worker's job) stay.  Returns the number removed."""
+    n = 0
+    for f in glob.glob(f"/dev/shm/{prefix}*"):
+        parts = os.path.basename(f).rsplit("-", 2)
+        if len(parts) != 3 or not parts[1].isdigit():
+            continue
+        try:
+            os.kill(int(parts[1]), 0)
+            continue  # the owner lives
+        except ProcessLookupError:
+            pass
+        except PermissionError:
+            continue
+        try:
+            os.unlink(f)
+            n += 1
+        except OSError:
+            pass
+    return n
+
+
 def kill_env(kills) -> str:
     """(rank, phase, step, point[, call]) tuples -> FTAR_KILL."""
     return ",".join(":".join(str(v) for v in k) for k in kills)
@@ -55,6 +79,9 @@ def wide(*cases):
     """Parametrize values that run only under FTAR_GPU_WIDE=1."""
     return list(cases) if WIDE else []
 GATES_ON = {"FTAR_GATE": "1", "FTAR_FLAG_SYNC": "1"}
+# the mesh's allgather after the reduce-scatter's host agree (not ordered on the device): the
+# form whose allgather launch a gate can queue behind the tree (FTAR_GATE_MAX >= S)
+HOST_AG = {"FTAR_MESH_WAIT": "0"}
 
 
 def run_probe(algo: str, inputs, kills=(), op: int = 0, iters: int = 1, backend: str = "hostsim",
@@ -71,9 +98,9 @@ def run_probe(algo: str, inputs, kills=(), op: int = 0, iters: int = 1, backend:
             hs = HOSTSIM if backend == "hostsim" else HOSTSIM_ASAN
             ftrun = os.path.join(hs, "bin", "ftrun")
             probe = os.path.join(hs, "bin", "ftar_probe")
-        else:
+        else:  # "gpu": the product library; "gpu_hooks": its TEST-ONLY hooks build (FTAR_KILL_WITHDRAW)
             ftrun = os.path.join(PKG, "bin", "ftrun")
-            probe = os.path.join(HOSTSIM, "gpu", "ftar_probe")
+            probe = os.path.join(HOSTSIM, "gpu_hooks" if backend == "gpu_hooks" else "gpu", "ftar_probe")
         env = dict(os.environ)
         tag = os.path.basename(tmp)
         env.update(FTAR_PROBE_DIR=tmp, FTAR_PROBE_ALGO=algo, FTAR_PROBE_DTYPE=str(dt),
@@ -123,13 +150,15 @@ def run_driver(which: str, nprocs: int, count: int, backend: str = "hostsim", ki
         env["FTAR_KILL"] = kill_env(kills)
     if env_extra:
         env.update(env_extra)
-    cp = subprocess.run([ftrun, "-np", str(nprocs), exe, str(count)], env=env, capture_output=True,
-                        text=True, timeout=timeout)
-    for f in glob.glob(f"/dev/shm/ftarhs-drv{os.getpid()}-*"):
-        try:
-            os.unlink(f)
-        except OSError:
-            pass
+    try:
+        cp = subprocess.run([ftrun, "-np", str(nprocs), exe, str(count)], env=env, capture_output=True,
+                            text=True, timeout=timeout)
+    finally:  # also on TimeoutExpired: every rank's fake device memory
+        for f in glob.glob(f"/dev/shm/ftarhs-drv{os.getpid()}-*"):
+            try:
+                os.unlink(f)
+            except OSError:
+                pass
     hello = {}
     for line in cp.stdout.splitlines():
         t = line.split()

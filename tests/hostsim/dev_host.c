@@ -12,12 +12,14 @@
 #define _GNU_SOURCE
 #endif
 #include <fcntl.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "../../fault-tolerant_amd/csrc/ftar_dev.h"
@@ -40,6 +42,8 @@ struct ftar_dev {
         fdev_seg segs[FDEV_MAX_SEGS];
     } gated;
     uint64_t gates_run, gates_skipped;
+    /* fdev_peer_wait: the next launch runs behind it (pw_pending), if the wait succeeded (pw_go) */
+    int pw_pending, pw_armed, pw_go, pw_abort;
     int flag_sync, tree_unroll; /* knobs: no flag path here; flag_sync = 0 turns the gates off, as on the GPU */
 };
 
@@ -132,19 +136,45 @@ static int put_map(void *p, size_t n, const char *name, int own)
     return -1;
 }
 
+/* "Device memory" is /dev/shm, which the whole container shares: every segment is backed
+ * when it is allocated (posix_fallocate), so exhaustion is an allocation error here -- the
+ * library then ends the job with FTAR_ERR_NOMEM -- and not a SIGBUS at the first touch of a
+ * page, which the job would see as a rank death.  FTAR_HOSTSIM_SHM_BUDGET=<bytes>
+ * (test-only) makes this process's allocations beyond that total fail the same way. */
 int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
 {
+    static size_t allocated;
     char name[64];
-    const char *tag = getenv("FTAR_HOSTSIM_TAG");
+    const char *tag = getenv("FTAR_HOSTSIM_TAG"), *budget = getenv("FTAR_HOSTSIM_SHM_BUDGET");
+    if (budget && allocated + bytes > (size_t)strtoull(budget, NULL, 10)) {
+        snprintf(g_err, sizeof(g_err), "out of shared memory: %zu B more than FTAR_HOSTSIM_SHM_BUDGET=%s allows",
+                 bytes, budget);
+        return 102;
+    }
     snprintf(name, sizeof(name), "/ftarhs-%s-%d-%d", tag ? tag : "x", (int)getpid(), g_seq++);
     int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) {
         snprintf(g_err, sizeof(g_err), "shm_open %s failed", name);
+        if (fd >= 0) {
+            close(fd);
+            shm_unlink(name);
+        }
         return 101;
+    }
+    int fe = bytes ? posix_fallocate(fd, 0, (off_t)bytes) : 0;
+    if (fe != 0) {
+        snprintf(g_err, sizeof(g_err), "out of shared memory: %zu B for %s (%s)", bytes, name, strerror(fe));
+        close(fd);
+        shm_unlink(name);
+        return 102;
     }
     void *p = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
-    if (p == MAP_FAILED) return 102;
+    if (p == MAP_FAILED) {
+        shm_unlink(name);
+        return 102;
+    }
+    allocated += bytes;
     memset(handle, 0, FDEV_HANDLE_BYTES);
     snprintf((char *)handle, FDEV_HANDLE_BYTES, "%s", name);
     put_map(p, bytes, name, 1);
@@ -269,10 +299,13 @@ static size_t esz(int dt) { return (dt == 0 || dt == 1) ? 4 : 8; }
 int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     if (d->gate_pending) fdev_gate_open(d, 1);
+    if (d->pw_pending) { /* behind a peer wait: runs only if every peer's flag arrived */
+        d->pw_pending = 0;
+        d->pw_armed = 1;
+        if (!d->pw_go) return 0;
+    }
     for (int k = 0; k < nseg; k++) {
         const fdev_seg *s = &segs[k];
-        int pre = s->out2 && s->out2_pre && s->kind != FDEV_COPY;
-        if (pre) memmove(s->out2, s->x, s->n * esz(dtype)); /* the pre-image, before an in-place reduce */
         if (s->kind == FDEV_COPY) {
             memmove(s->out, s->x, s->n * esz(dtype));
         } else {
@@ -283,7 +316,7 @@ int fdev_run(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int
             default: LOOP(double, op_f64); break;
             }
         }
-        if (s->out2 && !pre) memmove(s->out2, s->out, s->n * esz(dtype));
+        if (s->out2) memmove(s->out2, s->out, s->n * esz(dtype));
         if (s->remote & FDEV_REMOTE_OUT) d->ctr.link_bytes += (double)s->n * (double)esz(dtype);
     }
     d->ctr.launches[tag]++;
@@ -441,6 +474,47 @@ int fdev_gate_open(ftar_dev *d, int skip)
 
 int fdev_gate_pending(const ftar_dev *d) { return d->gate_pending; }
 
+/* host-sim: the flag is a word of the shared-memory W, the wait spins here on the host */
+int fdev_peer_wait(ftar_dev *d, void *flag, void *const *peer_flags, int npeers, uint64_t token,
+                   int (*poll)(void *), void *arg)
+{
+    if (!flag || npeers < 1 || npeers > FDEV_MAX_PEERS) return 13;
+    if (d->gate_pending) fdev_gate_open(d, 1);
+    __atomic_store_n((uint64_t *)flag, token, __ATOMIC_RELEASE);
+    d->pw_abort = d->pw_go = 0;
+    /* the device's give-up, as on the GPU: FTAR_GATE_TIMEOUT_MS (default 60 s) */
+    const char *gt = getenv("FTAR_GATE_TIMEOUT_MS");
+    const double limit = (gt ? atof(gt) : 60000.0) * 1e-3;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (;;) {
+        int all = 1;
+        for (int i = 0; i < npeers && all; i++) all = __atomic_load_n((const uint64_t *)peer_flags[i], __ATOMIC_ACQUIRE) >= token;
+        if (all) {
+            d->pw_go = 1;
+            break;
+        }
+        if (poll) poll(arg);
+        if (d->pw_abort) break;
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if ((double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec) > limit) break;
+        sched_yield();
+    }
+    d->pw_pending = 1;
+    d->pw_armed = 0;
+    return 0;
+}
+
+void fdev_peer_wait_abort(ftar_dev *d) { d->pw_abort = 1; }
+
+int fdev_peer_wait_verdict(ftar_dev *d)
+{
+    d->pw_pending = 0;
+    if (!d->pw_armed) return 1;
+    d->pw_armed = 0;
+    return d->pw_go;
+}
+
 int fdev_run_bg(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nseg, int tag)
 {
     return fdev_run(d, dtype, op, segs, nseg, tag);
@@ -469,25 +543,45 @@ int fdev_sync(ftar_dev *d, int (*poll)(void *), void *arg)
 int fdev_busy(ftar_dev *d) { return 0; } /* host "kernels" complete at launch */
 void fdev_fence_next_drain(ftar_dev *d) {}
 
+/* FTAR_HOSTSIM_FAIL_COPY=<rank>:<h2d|d2h>:<k> (test-only): that rank's k-th copy (0-based,
+ * counted over the process) in that direction fails, as a HIP copy error would */
+static int copy_fails(const char *dir)
+{
+    static int nh2d, nd2h;
+    int *n = dir[0] == 'h' ? &nh2d : &nd2h;
+    int k = (*n)++;
+    const char *e = getenv("FTAR_HOSTSIM_FAIL_COPY"), *me = getenv("FTAR_RANK");
+    int r, want;
+    char which[8];
+    if (!e || !me || sscanf(e, "%d:%7[a-z0-9]:%d", &r, which, &want) != 3) return 0;
+    if (r != atoi(me) || strcmp(which, dir) != 0 || k != want) return 0;
+    snprintf(g_err, sizeof(g_err), "injected %s copy failure (copy %d)", dir, k);
+    return 1;
+}
+
 int fdev_h2d(ftar_dev *d, void *dst, const void *src, size_t n)
 {
+    if (copy_fails("h2d")) return 101;
     memcpy(dst, src, n);
     return 0;
 }
 int fdev_h2d_async(ftar_dev *d, void *dst, const void *src, size_t n, int slot)
 {
+    if (copy_fails("h2d")) return 101;
     memcpy(dst, src, n);
     return 0;
 }
 int fdev_wait_h2d(ftar_dev *d, int slot, int (*poll)(void *), void *arg) { return poll ? poll(arg) : 0; }
 int fdev_d2h_async(ftar_dev *d, void *dst, const void *src, size_t n)
 {
+    if (copy_fails("d2h")) return 101;
     memcpy(dst, src, n);
     return 0;
 }
 int fdev_sync_d2h(ftar_dev *d, int (*poll)(void *), void *arg) { return poll ? poll(arg) : 0; }
 int fdev_d2h(ftar_dev *d, void *dst, const void *src, size_t n)
 {
+    if (copy_fails("d2h")) return 101;
     memcpy(dst, src, n);
     return 0;
 }

@@ -118,10 +118,10 @@ int main(void)
         fclose(f);
         snprintf(path, sizeof(path), "%s/status_%d_%d.txt", dir, rank, it);
         f = fopen(path, "w");
-        fprintf(f, "%d %d %d %d %lld %lld %lld %d %d %d %d %d %d %d %d\n", rc, crank, csize, st.recoveries,
+        fprintf(f, "%d %d %d %d %lld %lld %lld %d %d %d %d %d %d %d %d %d %d\n", rc, crank, csize, st.recoveries,
                 (long long)(st.wall_s * 1e6), (long long)(st.sync_wait_s * 1e6), (long long)(st.drain_s * 1e6), st.syncs,
                 st.relayed_steps, st.mesh_steps, st.gated_launches, st.gated_skips, st.step0_copy, st.gate_holds,
-                st.gate_relaunches);
+                st.gate_relaunches, st.peer_waits, st.peer_wait_skips);
         fclose(f);
     }
     ftar_finalize(comm);

@@ -3,8 +3,7 @@
 //
 // Random segment lists as the schedules build them -- up to 16 pieces of copies and
 // reduces, ragged lengths, element offsets that are co-aligned or not (vector body with
-// scalar head / tail, or the scalar path), a second destination (the result again, or for a
-// reduce the pre-image of its local operand: the mid-exchange guard, fdev_seg.out2_pre) --
+// scalar head / tail, or the scalar path), a second destination receiving the result again --
 // planned by plan_segments at several grid caps (one tile per workgroup, and capped grids
 // whose workgroups loop, as the mid-size gated launches run) and launched by
 // launch_segments.  Expected values: copies as they are, reduces by the oracle's
@@ -107,7 +106,7 @@ int main(int argc, char **argv)
             const size_t n = g() % 8 == 0 ? (size_t)(g() % (1u << 20)) + 1 : (size_t)(g() % 9000) + 1;
             auto off = [&]() { return coalign ? common : (size_t)(g() % 4) * es % 16; };
             const int kind = g() % 3 == 0 ? ftar::kCopy : ftar::kReduce;
-            const int with2 = (int)(g() % 3); // 0 none, 1 the result again, 2 (reduce) the pre-image
+            const bool with2 = g() % 3 != 0; // a second destination: the result again
             hx[s].resize(n * es);
             hy[s].resize(n * es);
             fill(hx[s].data(), dt, op, n, g);
@@ -124,14 +123,13 @@ int main(int argc, char **argv)
             in[s].y = kind == ftar::kCopy ? nullptr : ys.back().ptr();
             in[s].n = n;
             in[s].out2 = with2 ? out2s.back().ptr() : nullptr;
-            in[s].out2_pre = with2 == 2 && kind == ftar::kReduce;
             want[s] = swapped && kind == ftar::kReduce ? hy[s] : hx[s];
             if (kind == ftar::kReduce &&
                 ftar_oracle_reduce_local(dt, op, (swapped ? hx[s] : hy[s]).data(), want[s].data(), n) != 0) {
                 fprintf(stderr, "oracle refused dtype %d op %d\n", dt, op);
                 return 2;
             }
-            want2[s] = in[s].out2_pre ? hx[s] : want[s];
+            want2[s] = want[s];
         }
         ftar::KSegList L;
         const unsigned grid = ftar::plan_segments(in.data(), nseg, es, cap, &L);
@@ -154,7 +152,7 @@ int main(int argc, char **argv)
                     while (e < n && !memcmp(whole.data() + Buf::kPad + b.off + e * es, w.data() + e * es, es)) e++;
                     printf("FAIL list %d piece %d/%d (%s, n %zu, dtype %d op %d, cap %u, %s%s): element %zu\n", li, s,
                            nseg, in[s].kind == ftar::kCopy ? "copy" : "reduce", n, dt, op, cap,
-                           which ? (in[s].out2_pre ? "pre-image destination" : "second destination") : "out",
+                           which ? "second destination" : "out",
                            coalign ? ", co-aligned" : "", e);
                     ok = false;
                 }

@@ -53,7 +53,6 @@ int main(int argc, char **argv)
             in[i].y = (const void *)(base + ((uintptr_t)2 << 36) + mis_o);
             in[i].n = n;
             in[i].out2 = (rnd() % 4 == 0) ? (void *)(base + ((uintptr_t)3 << 36) + mis_o) : nullptr;
-            in[i].out2_pre = in[i].out2 && in[i].kind == kReduce && (rnd() & 1);
         }
         unsigned max_blocks = (rnd() % 5 == 0) ? 64 + (unsigned)(rnd() % 2048) : 262144;
         KSegList L;

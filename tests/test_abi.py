@@ -154,3 +154,49 @@ def test_python_structs_mirror_the_header(tmp_path):
         assert int(got[cname]) == ctypes.sizeof(cls), cname
         for f in cfields:
             assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
+
+
+def test_test_hooks_are_not_in_the_product(built):
+    """The test-only switches (FTAR_TRACE_DROP: a drain without its release; FTAR_KILL_WITHDRAW:
+    a dying rank rewrites the control block) are compiled only into the TEST-ONLY hooks build
+    (lib/libftar_hooks.so, -DFTAR_TEST_HOOKS) that the GPU tests needing them load; the product
+    library does not contain them, and both export the same C ABI (VERDICT r05 next #6)."""
+    hooks = os.path.join(ROOT, "fault-tolerant_amd", "lib", "libftar_hooks.so")
+    prod = open(built, "rb").read()
+    for name in (b"FTAR_TRACE_DROP", b"FTAR_KILL_WITHDRAW"):
+        assert name not in prod, name
+        assert name in open(hooks, "rb").read(), name
+    assert exported_symbols(hooks) == exported_symbols(built) == declared_functions()
+
+
+def _tree_src_id():
+    return subprocess.run([os.path.join(ROOT, "fault-tolerant_amd", "tools", "build_id.sh"), "src"],
+                          capture_output=True, text=True, check=True).stdout.strip()
+
+
+def test_library_is_built_from_this_tree(built):
+    """ftar_build_id() carries the digest of every product source the library was linked from:
+    after make it is the digest of the tree's sources, so a result of this library is a result
+    of this tree (VERDICT r05 next #3)."""
+    L = ctypes.CDLL(built)
+    L.ftar_build_id.restype = ctypes.c_char_p
+    got = L.ftar_build_id().decode()
+    assert re.fullmatch(r"ftar-build abi=[0-9a-f]{16} src=[0-9a-f]{16}", got), got
+    assert got.endswith("src=" + _tree_src_id())
+
+
+def test_stale_launcher_is_refused(hostsim, tmp_path):
+    """A launcher built from other headers than the library (a stale ftrun next to a new
+    libftar): the rank refuses to attach with one line naming both builds, and the job ends
+    instead of running with mismatched control-block layouts (VERDICT r05 next #3)."""
+    pkg = os.path.join(ROOT, "fault-tolerant_amd")
+    stale = tmp_path / "ftrun_stale"
+    subprocess.run(["gcc", "-O1", "-std=c11", "-D_GNU_SOURCE", "-DFTAR_ABI_ID=0x1234abcdull", "-o", str(stale),
+                    os.path.join(pkg, "tools", "ftrun.c"), os.path.join(pkg, "csrc", "ftar_ctrl.c"),
+                    "-lpthread", "-lrt"], check=True)
+    env = dict(os.environ, FTAR_HOSTSIM_TAG=f"stale{os.getpid()}", FTAR_PROBE_DIR=str(tmp_path),
+               FTAR_PROBE_ALGO="raben", FTAR_PROBE_COUNT="16", FTAR_PROBE_DTYPE="0")
+    cp = subprocess.run([str(stale), "-np", "2", os.path.join(hostsim, "bin", "ftar_probe")], env=env,
+                        capture_output=True, text=True, timeout=60)
+    assert cp.returncode != 0
+    assert "created by build 000000001234abcd" in cp.stderr and "different builds" in cp.stderr, cp.stderr[-1500:]

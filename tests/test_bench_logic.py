@@ -434,6 +434,10 @@ def test_bench_multi_four_ranks_gated_allgather(hostsim, tmp_path):
     assert fin["transports"]["mesh_gated_ag"]["plain_gated_launches"] > 0, fin["transports"]["mesh_gated_ag"]
     nd = fin["node_decisions"]
     assert nd["gated_ag_faster"] in (True, False), nd
+    # the device-ordered allgather (default) against the host-agree form: timed, exact, decided
+    assert "mesh_host_ag_ms" in sel and fin["exact_on_node"]["mesh_host_ag"], (sel, fin["exact_on_node"])
+    assert nd["device_wait_faster"] in (True, False), nd
+    assert "mesh_host_ag" in fin["transports"], fin["transports"]
     rl = fin["rd"]["schedule_link_roofline"]
     assert rl["reference_bytes_per_rank"] == 2.0 * 4 * (1 << 20), rl
     assert "non_kernel_ms" in fin["north_star"], fin["north_star"]

@@ -88,15 +88,17 @@ def test_run_compare_campaign_gpu(tmp_path):
     """All four executables on the GPU (NP = 1: the box has one GPU and RCCL refuses two
     ranks on one device), including the RCCL vendor baseline.  The inputs are rank + 5
     (FTAR_FILL_OFFSET), so every RESULT is the nonzero closed form 5 * SIZE, not the 0 a
-    one-rank run of the reference's input gives whatever the drivers compute."""
-    env = dict(os.environ, FTAR_CMP_NPS="1", FTAR_CMP_BUF_MIN="1", FTAR_CMP_BUF_MAX="1",
+    one-rank run of the reference's input gives whatever the drivers compute.  Two sizes: one
+    int and 2^20 ints (4 MiB, past every small-call path) -- ADVICE r05."""
+    env = dict(os.environ, FTAR_CMP_NPS="1", FTAR_CMP_BUF_MIN="1", FTAR_CMP_BUF_MAX=str(1 << 20),
+               FTAR_CMP_BUF_MUL=str(1 << 20),
                FTAR_CMP_OUT=str(tmp_path / "out"), FTAR_CMP_DATA=str(tmp_path / "data"), FTAR_FILL_OFFSET="5")
     os.makedirs(tmp_path / "out")
     cp = subprocess.run(["./run_compare.sh", "1"], cwd=RUN, env=env, capture_output=True, text=True, timeout=600)
     assert cp.returncode == 0, cp.stdout[-2000:] + cp.stderr[-2000:]
     for name in ("rd", "original_rd", "raben", "original_raben"):
         rows = _rows(tmp_path / "data" / f"{name}.csv")
-        assert len(rows) == 1, (name, rows, cp.stdout[-2000:])
+        assert sorted(int(r["SIZE"]) for r in rows) == [1, 1 << 20], (name, rows, cp.stdout[-2000:])
         assert all(int(r["RESULT"]) == 5 * int(r["SIZE"]) and int(r["SIZE"]) > 0 for r in rows), rows
 
 

@@ -68,8 +68,8 @@ def test_missing_acquire_is_caught(tmp_path):
 def test_gated_launch_runs_at_its_gate(tmp_path):
     """A gated launch's body runs when its gate opens (G go), after the barrier; a skipped
     one never runs; the staging phase before the gate is released by its own flag."""
-    def rank(me, peer, skip=False):
-        return [L(1, w=f"{me}:IN:0:128,", r=f"{peer}:IN:0:128,", sig=2, acq=1, gate=1, sw=f"{me}:IN:0:128,", stag=1),
+    def rank(me, peer, skip=False):  # the one-shot form: stages IN, then reads the peer's IN into rbuf
+        return [L(1, r=f"{peer}:IN:0:128,", sig=2, acq=1, gate=1, sw=f"{me}:IN:0:128,", stag=1),
                 "D sig 1", "A 1", "P 1", f"G 1 {'skip' if skip else 'go'}", "D sig 2", "A 2", "P 2"]
     rep = FC.check_prefix(_write(str(tmp_path), {0: rank(0, 1), 1: rank(1, 0)}))
     assert rep.ok and rep.reads_checked == 2, (rep.release, rep.acquire)
@@ -91,3 +91,53 @@ def test_dead_rank_reads(tmp_path):
     live[-1] = L(5, r="1:W:0:64,")  # the dead rank's unreleased in-flight step read
     rep = FC.check_prefix(_write(str(tmp_path), {0: live, 1: dead}))
     assert rep.release and "after its last arrival" in rep.release[0], rep.release
+
+
+def _devwait_call(me, peer, k0, pub="M pub", wait=True, tok=None):
+    """The mesh with the allgather ordered on the device (fdev_peer_wait): stage, barrier k0,
+    tree into my W block, fenced marker + flag F, wait V for the peer's flag, allgather of the
+    peer's W block behind a fenced marker, drain, barrier k0 + 1."""
+    mine, theirs = 64 * me, 64 * peer
+    tok = k0 if tok is None else tok
+    lines = [L(1, w=f"{me}:IN:0:128,", sig=1), "D sig 1", f"A {k0}", f"P {k0}",
+             L(2, r=f"{me}:IN:{mine}:64,{peer}:IN:{mine}:64,", w=f"{me}:W:{mine}:64,")]
+    if pub:
+        lines.append(pub)
+    lines += [f"F {k0} w={me}:W:4096:8,"]
+    if wait:
+        lines.append(f"V {tok} r={peer}:W:4096:8,")
+    lines += [L(3, r=f"{peer}:W:{theirs}:64,", fence=1), "D mk m", f"A {k0 + 1}", f"P {k0 + 1}"]
+    return lines
+
+
+def test_device_wait_orders_the_allgather(tmp_path):
+    """The allgather reads the peer's block written in the same round: fine behind a wait for
+    the peer's flag that a fenced marker released the tree in front of."""
+    rep = FC.check_prefix(_write(str(tmp_path), {0: _devwait_call(0, 1, 1), 1: _devwait_call(1, 0, 1)}))
+    assert rep.ok, (rep.release, rep.acquire)
+    assert rep.reads_checked >= 4
+
+
+def test_device_wait_without_release_is_caught(tmp_path):
+    """FTAR_TRACE_DROP=release on the flag's marker: the tree was not released before the flag."""
+    rep = FC.check_prefix(_write(str(tmp_path), {0: _devwait_call(0, 1, 1), 1: _devwait_call(1, 0, 1, pub=None)}))
+    assert rep.release and "no fenced marker released it before flag" in rep.release[0], rep.release
+
+
+def test_same_round_read_without_wait_is_a_race(tmp_path):
+    """The allgather queued without the wait (no V): it reads what the peer writes in the same
+    round -- a race the barrier rule alone never sees."""
+    rep = FC.check_prefix(_write(str(tmp_path), {0: _devwait_call(0, 1, 1, wait=False), 1: _devwait_call(1, 0, 1)}))
+    assert rep.release and "in the same round, with no wait" in rep.release[0], rep.release
+    # a wait for a token the peer never published
+    rep = FC.check_prefix(_write(str(tmp_path), {0: _devwait_call(0, 1, 1, tok=7), 1: _devwait_call(1, 0, 1)}))
+    assert rep.release and "never published" in rep.release[0], rep.release
+
+
+def test_skipped_launch_reads_nothing(tmp_path):
+    """A launch behind a wait that was given up (S n) returned untouched: nothing it would
+    have read is checked."""
+    r0 = _devwait_call(0, 1, 1, wait=False)
+    r0.insert(r0.index("D mk m") + 1, "S 3")
+    rep = FC.check_prefix(_write(str(tmp_path), {0: r0, 1: _devwait_call(1, 0, 1)}))
+    assert rep.ok, rep.release

@@ -33,13 +33,15 @@ BASE = [
     (4, "raben", 16384, {}),                               # 64 KiB one-shot
     (4, "raben", 262140, {}),                              # 1 MiB - 16 B
     (4, "raben", 262148, {}),                              # 1 MiB + 16 B: two-launch mesh, read in place
-    (4, "raben", MIB, {}),                                 # 4 MiB mesh
+    (4, "raben", MIB, {}),                                 # 4 MiB mesh (allgather behind a device wait)
+    (4, "raben", MIB, {"FTAR_MESH_WAIT": "0"}),            # 4 MiB mesh, allgather after a host agree
+    (16, "raben", MIB, {}),                                # 16-source tree, 15 flags per wait
     (4, "raben", MIB, {"FTAR_TREE_UNROLL": "2"}),          # mesh_u2
     (8, "raben", MIB, {"FTAR_TREE_UNROLL": "4"}),          # mesh_u4, 8 ranks
     (4, "raben", MIB, {"FTAR_PUSH": "1"}),                 # mesh_push
     (4, "raben", MIB, {"FTAR_PUSH": "2"}),                 # mesh_push2
     (4, "raben", 16384, {"FTAR_PUSH": "2", "FTAR_ONESHOT_MAX": "0"}),
-    (4, "raben", MIB, {"FTAR_GATE_MAX": str(16 * MIB)}),   # mid-size gate: allgather behind the tree
+    (4, "raben", MIB, {"FTAR_GATE_MAX": str(16 * MIB), "FTAR_MESH_WAIT": "0"}),  # mid-size gate: allgather behind the tree
     (4, "raben", MIB, {"FTAR_MESH": "0", "FTAR_RELAY": "1", "FTAR_RELAY_MIN": "0"}),  # relay2hop
     (4, "raben", MIB, {"FTAR_MESH": "0", "FTAR_RELAY": "0"}),                         # direct
     (4, "raben", MIB, {"FTAR_MESH": "0", "FTAR_COPY_ENGINE": "1"}),                   # copy engine
@@ -59,7 +61,7 @@ BASE = [
     (5, "raben", MIB, {"FTAR_KILL": "4:2:0:3:1"}),         # last AG step, DURING
     (5, "rd", 16384, {"FTAR_KILL": "1:1:1:3:1"}),          # RD step 1, DURING
     (4, "raben", 64 * MIB, {}),                            # 256 MiB mesh
-    (4, "raben", 64 * MIB, {"FTAR_GATE_MAX": str(256 * MIB)}),  # mesh_gated_ag at the headline size
+    (4, "raben", 64 * MIB, {"FTAR_GATE_MAX": str(256 * MIB), "FTAR_MESH_WAIT": "0"}),  # mesh_gated_ag, headline size
 ]
 WIDE = [
     (8, "raben", 1, {}), (8, "raben", 16384, {}), (8, "raben", 262140, {}), (8, "raben", 262148, {}),
@@ -75,10 +77,11 @@ def _trace_job(p, algo, n, opts, drop=None, calls=3):
     # pattern inputs (every element its own exact sum) without kills; rank ids with one
     env = {k: v for k, v in os.environ.items() if k not in ("FTAR_KILL", "FTAR_TRACE_DROP")}
     env.update(opts, FTBENCH_PATTERN="0" if "FTAR_KILL" in opts else "1", FTAR_TRACE=os.path.join(tmp, "t"))
-    if drop:
+    if drop:  # the drop hook lives only in the TEST-ONLY hooks build of the library
         env["FTAR_TRACE_DROP"] = drop
+    bench = "ftbench_hooks" if drop else "ftbench"
     cp = subprocess.run([os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ",".join("0" * p),
-                         os.path.join(H.PKG, "bin", "ftbench"), algo, str(n), str(calls)], env=env,
+                         os.path.join(H.PKG, "bin", bench), algo, str(n), str(calls)], env=env,
                         capture_output=True, text=True, timeout=240)
     lines = [json.loads(ln) for ln in cp.stdout.splitlines() if ln.startswith("{")]
     logs = FC.load(os.path.join(tmp, "t"))
@@ -126,12 +129,16 @@ def test_fence_discipline(p, algo, n, opts):
 
 
 @pytest.mark.timeout(300)
-def test_dropped_release_fails_the_check():
-    """The mesh's tree is drained by a fenced marker before the reduce-scatter's barrier; with
-    that marker's system fence removed (test-only switch) the allgather's peer reads of the
-    blocks it wrote are unreleased reads, and the checker says so."""
-    rep, _ = _trace_job(4, "raben", MIB, {}, drop="release")
+@pytest.mark.parametrize("wait", ["1", "0"])
+def test_dropped_release_fails_the_check(wait):
+    """The mesh's tree is released by a fenced marker -- in front of the flag the peers'
+    allgathers wait for on the device (FTAR_MESH_WAIT=1), or drained before the reduce-scatter's
+    barrier (0); with that marker's system fence removed (test-only switch) the allgather's
+    peer reads of the blocks it wrote are unreleased reads, and the checker says so."""
+    rep, _ = _trace_job(4, "raben", MIB, {"FTAR_MESH_WAIT": wait}, drop="release")
     assert rep.release, "a removed release went unnoticed"
+    if wait == "1":
+        assert any("before flag" in v for v in rep.release), rep.release[:3]
 
 
 @pytest.mark.timeout(300)

@@ -31,7 +31,7 @@ def _run(oracle, algo, p, env, iters=3, count=1031):
     # the next launch is gated)
     late = {"FTAR_PROBE_RANK_ENV": f"{p - 1}:FTAR_PROBE_SLEEP_US=300000" if count <= 4096 else
             f"{p - 1}:FTAR_LOOP_SECONDS=0.3", "FTAR_RELAY": "0", "FTAR_HOST_PIPE": "0", "FTAR_GATE_MAX": str(16 << 20),
-            **H.MESH_FORM, **H.GATES_ON}  # the pull mesh: its allgather is what a mid-size call gates
+            **H.MESH_FORM, **H.GATES_ON, **H.HOST_AG}  # the pull mesh: its allgather is what a mid-size call gates
     r = H.run_probe(algo, ins, iters=iters, backend="gpu", devmap=ALL_ON_GPU0, timeout=120, env_extra=dict(late, **env))
     assert r.returncode == 0 and not r.aborted, r.stderr[-2000:]
     for w in range(p):
@@ -68,7 +68,8 @@ def test_mid_size_gates(oracle, algo, p, count):
     o = oracle.rabenseifner(ins, op=2) if algo == "raben" else oracle.recursive_doubling(ins, op=2)
     r = H.run_probe(algo, ins, op=2, iters=3, backend="gpu", devmap=ALL_ON_GPU0, timeout=200,
                     env_extra={"FTAR_RELAY": "0", "FTAR_ONESHOT_MAX": "0", "FTAR_HOST_PIPE": "0", **H.MESH_FORM,
-                               **H.GATES_ON, "FTAR_GATE_TIMEOUT_MS": "10000", "FTAR_GATE_MAX": str(16 << 20)})
+                               **H.GATES_ON, **H.HOST_AG, "FTAR_GATE_TIMEOUT_MS": "10000",
+                               "FTAR_GATE_MAX": str(16 << 20)})
     assert r.returncode == 0 and not r.aborted, r.stderr[-2000:]
     per_call = (p.bit_length() - 2) if algo == "rd" else 1
     for w in range(p):

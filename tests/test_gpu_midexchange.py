@@ -32,7 +32,9 @@ REFERENCE_SHAPE = {"FTAR_MESH": "0", "FTAR_REDUNDANCY": "1", "FTAR_OVERLAP": "0"
 
 def _check(fn, algo, inputs, kills=(), op=0, env=None, timeout=300):
     o = fn(inputs, kills, op=op)
-    r = H.run_probe(algo, inputs, kills, op=op, backend="gpu", devmap=ALL_ON_GPU0, timeout=timeout,
+    # the withdrawal hook lives only in the TEST-ONLY hooks build of the library
+    backend = "gpu_hooks" if env and "FTAR_KILL_WITHDRAW" in env else "gpu"
+    r = H.run_probe(algo, inputs, kills, op=op, backend=backend, devmap=ALL_ON_GPU0, timeout=timeout,
                     env_extra=env)
     u = {4: np.uint32, 8: np.uint64}[inputs[0].dtype.itemsize]
     if o.aborted:

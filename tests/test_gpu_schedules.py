@@ -157,6 +157,26 @@ def test_driver_golden_checksums(algo, p):
         assert set(hello.values()) == {want}, (size, hello, want)
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("algo", ["raben", "rd"])
+@pytest.mark.parametrize("p", [12, 16])
+def test_driver_golden_checksums_np_grid(algo, p):
+    """The reference's own NP grid on the GPU (run/run_test.sh draws N in [4, 32]; its
+    data_compare rows go up to NP = 64): the drop-in drivers at NP = 12 (Raben with 4 pre-step
+    pairs, RD's reduce_pow2 over 4 extra ranks) and NP = 16 (the 16-source mesh tree, RD over
+    4 steps) -- 12 / 16 rank processes time-sliced on one GPU, each with its own HIP context
+    and 4 x (NP - 1) IPC imports -- every rank's checksum equal to the reference's RESULT at
+    1, 16384 and 2^20 ints.  NP = 16 is the box's cap on processes that
+    use the GPU at once; the host-sim covers NP up to 64 (tests/test_hostsim.py)."""
+    gold = _golden_checksums()
+    for size in (1, 16384, 1 << 20):
+        want = gold[(algo, p, size)]
+        cp, hello = H.run_driver(algo, p, size, backend="gpu", env_extra={"FTAR_DEVMAP": ALL_ON_GPU0}, timeout=240)
+        assert cp.returncode == 0, (size, cp.stderr[-2000:])
+        assert sorted(hello) == list(range(p)), (size, cp.stdout[-1000:])
+        assert set(hello.values()) == {want}, (size, hello, want)
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("algo", ["raben", "rd"])
 @pytest.mark.parametrize("p", [4, 8])
@@ -257,15 +277,20 @@ def test_raben_redundancy_always(oracle, p, kill):
 
 
 @pytest.mark.parametrize("algo,p,mode", [("raben", 4, "plain"), ("raben", 8, "inplace_offset3"), ("raben", 3, "inplace"),
-                                         ("rd", 4, "offset1")] +
+                                         ("rd", 4, "offset1"), ("raben", 4, "inplace_mesh")] +
                          H.wide(("raben", 4, "inplace"), ("raben", 2, "offset1"), ("rd", 4, "inplace")))
 def test_torch_device_buffers(oracle, algo, p, mode):
     """The device-pointer entry points on torch tensors (bench.py's path), bound through
-    the Python package: in place, at element offsets, two calls; sbuf untouched."""
+    the Python package: in place, at element offsets, two calls; sbuf untouched.
+    inplace_mesh: the two-launch mesh in place on device memory past the one-shot range (2 MiB),
+    where the tree also stores this rank's final block into rbuf -- here sbuf -- while the
+    peers read their blocks of it."""
     env = {"plain": {}, "inplace": {"FTAR_PROBE_INPLACE": "1"}, "offset1": {"FTAR_PROBE_OFFSET": "1"},
-           "inplace_offset3": {"FTAR_PROBE_INPLACE": "1", "FTAR_PROBE_OFFSET": "3"}}[mode]
+           "inplace_offset3": {"FTAR_PROBE_INPLACE": "1", "FTAR_PROBE_OFFSET": "3"},
+           "inplace_mesh": dict(H.MESH_FORM, FTAR_PROBE_INPLACE="1", FTAR_ONESHOT_MAX="0")}[mode]
     env = dict(env, FTAR_STAGE_MAX="0")  # peers read sbuf in place (the path above 1 MiB)
-    ins = oracle.random_inputs(p, 65536 + 17, seed=p + 90)
+    count = (1 << 19) + 64 if mode == "inplace_mesh" else 65536 + 17
+    ins = oracle.random_inputs(p, count, seed=p + 90)
     o = (oracle.rabenseifner if algo == "raben" else oracle.recursive_doubling)(ins)
     r = H.run_torch_worker(algo, ins, devmap=ALL_ON_GPU0, env_extra=env)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -274,6 +299,58 @@ def test_torch_device_buffers(oracle, algo, p, mode):
         for it in range(2):
             assert r.status[w][it] == (0, 1), (w, it, r.status[w][it])
             assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+
+
+@pytest.mark.parametrize("p", [4, 8])
+def test_mesh_peer_wait(oracle, p):
+    """The mesh's allgather ordered behind the peers' trees on the device (FTAR_OPT_MESH_WAIT,
+    the default): one peer wait per call, none given up, one agree round fewer than the
+    allgather after a host agree (FTAR_MESH_WAIT=0), bit-identical results (MAX over NaN /
+    signed zeros pins every combination's operand order), two calls."""
+    ins = H.with_specials(oracle.random_inputs(p, (1 << 20) + 3, seed=p + 170), p)
+    o = oracle.rabenseifner(ins, op=2)
+    runs = {}
+    for wait in ("1", "0"):
+        r = H.run_probe("raben", ins, op=2, iters=2, backend="gpu", devmap=ALL_ON_GPU0, timeout=300,
+                        env_extra=dict(H.MESH_FORM, FTAR_ONESHOT_MAX="0", FTAR_MESH_WAIT=wait))
+        assert r.returncode == 0, r.stderr[-2000:]
+        for w in range(p):
+            for it in range(2):
+                assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (wait, w, it)
+                assert r.status[w][it][15] == (1 if wait == "1" else 0) and r.status[w][it][16] == 0, r.status[w]
+        runs[wait] = r
+    assert all(runs["1"].status[w][0][7] == runs["0"].status[w][0][7] - 1 for w in range(p))
+
+
+def test_mesh_peer_wait_timeout_fallback(oracle):
+    """A rank publishes its flag 300 ms late (test hook, the hooks build): its peers' wait
+    kernels give up after FTAR_GATE_TIMEOUT_MS and their allgathers return untouched; the
+    verdicts travel in the last agree round, those ranks launch the allgather again -- exact
+    results, the late rank's own wait not given up."""
+    p, late = 4, 2
+    ins = oracle.random_inputs(p, (1 << 20) + 3, seed=175)
+    o = oracle.rabenseifner(ins)
+    r = H.run_probe("raben", ins, iters=2, backend="gpu_hooks", devmap=ALL_ON_GPU0, timeout=300,
+                    env_extra=dict(H.MESH_FORM, FTAR_ONESHOT_MAX="0", FTAR_GATE_TIMEOUT_MS="30",
+                                   FTAR_PROBE_RANK_ENV=f"{late}:FTAR_PEER_WAIT_DELAY_US=300000"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    for w in range(p):
+        for it in range(2):
+            assert np.array_equal(r.outputs[w][it].view(np.uint32), o.outputs[w].view(np.uint32)), (w, it)
+            assert r.status[w][it][16] == (0 if w == late else 1), (w, it, r.status[w][it])
+
+
+@pytest.mark.parametrize("kill", [(2, 1, 0, 0), (1, 1, 1, 3), (0, 2, 1, 3), (3, 2, 0, 1)])
+def test_mesh_peer_wait_kills_abort(oracle, kill):
+    """Kills around the device wait (p = 4, no idle rank: every failure aborts): before the
+    tree -- the victim never publishes, the peers' wait kernels are given up by their failure
+    detectors through the abort word --, with the tree in flight, during and after the
+    allgather: a clean abort each time, never a hang."""
+    ins = oracle.random_inputs(4, (1 << 20) + 3, seed=180 + kill[0])
+    assert oracle.rabenseifner(ins, [kill]).aborted
+    r = H.run_probe("raben", ins, [kill], backend="gpu", devmap=ALL_ON_GPU0, timeout=120,
+                    env_extra=dict(H.MESH_FORM, FTAR_ONESHOT_MAX="0"))
+    assert r.aborted and not r.outputs, r.stderr[-2000:]
 
 
 MESH_SHAPES = [(2, 0, 100003), (4, 0, 100003), (8, 0, 65536 + 5), (4, 2, 4099), (8, 3, 4099), (4, 0, (1 << 22) + 13),

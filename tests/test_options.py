@@ -55,19 +55,25 @@ def test_option_errors(solo):
     assert L.ftar_comm_get_option(h, 99, ctypes.byref(v)) == 13
 
 
-def test_env_redundancy_out_of_range_is_refused(hostsim, monkeypatch):
+@pytest.mark.parametrize("value,want", [("3", "13"), ("-1", "13"), ("auto", "13"), ("on", "13"), ("", "13"),
+                                        ("1x", "13"), ("0", "0"), ("1", "0"), ("2", "0")])
+def test_env_redundancy_out_of_range_is_refused(hostsim, monkeypatch, value, want):
     """FTAR_REDUNDANCY in the environment accepts what ftar_comm_set_option accepts (0, 1, 2):
-    a typo such as 3 is refused with FTAR_ERR_ARG and a message, never silently taken as auto
-    (ADVICE r04)."""
+    a typo such as 3 -- or a word such as 'auto', which atoi would have read as 0 and so turned
+    the step-0 copy off -- is refused with FTAR_ERR_ARG and a message."""
     import subprocess
     import sys
     code = ("import ctypes, os\n"
             f"L = ctypes.CDLL({os.path.join(hostsim, 'libftar_hostsim.so')!r})\n"
             "L.ftar_init_rank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_int, ctypes.c_int,"
             " ctypes.c_int]\n"
+            "L.ftar_finalize.argtypes = [ctypes.c_void_p]\n"
             "h = ctypes.c_void_p()\n"
-            "print(L.ftar_init_rank(ctypes.byref(h), b'/ftar-optenv-%d' % os.getpid(), 0, 1, 0))\n")
-    env = dict(os.environ, FTAR_REDUNDANCY="3", FTAR_HOSTSIM_TAG=f"optenv{os.getpid()}")
+            "rc = L.ftar_init_rank(ctypes.byref(h), b'/ftar-optenv-%d' % os.getpid(), 0, 1, 0)\n"
+            "print(rc)\n"
+            "if rc == 0: L.ftar_finalize(h)\n")
+    env = dict(os.environ, FTAR_REDUNDANCY=value, FTAR_HOSTSIM_TAG=f"optenv{os.getpid()}")
     cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=60)
-    assert cp.stdout.strip() == "13", (cp.stdout, cp.stderr)
-    assert "FTAR_REDUNDANCY=3" in cp.stderr and "refused" in cp.stderr
+    assert cp.stdout.strip() == want, (cp.stdout, cp.stderr)
+    if want != "0":
+        assert f"FTAR_REDUNDANCY={value} " in cp.stderr and "refused" in cp.stderr
