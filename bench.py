@@ -1559,9 +1559,16 @@ def multi(args):
                         comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)
                     lb = timed.link_bytes
                     tv_rd = timed(rd)[0] if name in ("relay2hop", "direct", "copy_engine") else None
+                    bd = timed_split.breakdown
                     out[name] = {"raben_ms": round(tv * 1e3, 4), "raben_algbw_GBps": round(S / tv / 1e9, 2),
                                  "step0_kernel_ms": round(kv, 4), "step0_link_bytes": lb,
-                                 "step0_pull_GBps": round(lb / (kv * 1e-3) / 1e9, 2) if kv > 0 else None}
+                                 "step0_pull_GBps": round(lb / (kv * 1e-3) / 1e9, 2) if kv > 0 else None,
+                                 # the call's time outside its kernels (plain call - profiled kernels)
+                                 "kernels_ms": bd.get("kernels_ms"),
+                                 "non_kernel_ms": round(bd["plain_call_ms"] - bd["kernels_ms"], 4)
+                                 if bd.get("plain_call_ms") is not None and bd.get("kernels_ms") is not None else None,
+                                 "agree_barrier_wait_ms": bd.get("agree_barrier_wait_ms"),
+                                 "peer_waits": bd.get("peer_waits")}
                     if tv_rd:
                         out[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
                     if name == "mesh_gated_ag":

@@ -698,13 +698,11 @@ static int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg
     L.nt_store = nt_store();
     note_launch(d, st, grid, true, &L.sig);
     if (behind_wait) {
-        // behind a peer wait: a fenced marker first (device-wide acquire: the peers' data read
-        // fresh, not from lines this GPU cached before), then the wait's verdict decides
-        if (!d->tr_fenced && d->tr_drop != 2) { // tr_drop 2: TEST-ONLY, acquires left out
-            HIPCHK(hipEventRecord(d->fence_main, st));
-            d->tr_fenced = 1;
-        }
-        d->need_acquire = 0;
+        // behind a peer wait: the wait's verdict decides.  No acquire of its own: the fenced
+        // marker in front of the flag (fdev_peer_wait) invalidated this GPU's caches after
+        // everything this rank read before, and since then only the wait kernel has read peer
+        // memory (the flag words, a page of their own) -- no line of what this launch reads can
+        // be stale (tests/fence_check.py's acquire rule checks exactly that on the logs)
         L.sig.vword = d->gate_dw + 48;
         L.sig.vval = d->pw_vval;
         d->pw_armed = 1;
@@ -1432,7 +1430,7 @@ int fdev_peer_wait(ftar_dev *d, void *flag, void *const *peer_flags, int npeers,
     hipError_t e = ftar::launch_peer_wait(W, d->stream);
     if (e != hipSuccess) return set_err(e, "peer_wait_kernel launch");
     d->unsignalled++; // drained through a fenced marker
-    d->need_acquire = 0;
+    d->need_acquire = d->tr_drop == 1; // the marker invalidated the caches (unless it was dropped)
     d->pw_pending = 1;
     d->pw_armed = 0;
     return 0;
