@@ -68,7 +68,7 @@ def kill_env(kills) -> str:
 # than only the result: the suite runs under any FTAR_MESH / FTAR_PUSH / FTAR_TREE_UNROLL / FTAR_GATE
 # setting of its environment -- e.g. the node's chosen transport made the default -- and only the
 # tests that say which form they check pin it.
-MESH_FORM = {"FTAR_MESH": "1", "FTAR_PUSH": "0", "FTAR_TREE_UNROLL": "1"}
+MESH_FORM = {"FTAR_MESH": "1", "FTAR_PUSH": "0", "FTAR_TREE_UNROLL": "1", "FTAR_MESH_WAIT": "1"}
 # FTAR_GPU_WIDE=1: the GPU suite's repeats of a shape already covered once (more forms, seeds,
 # sizes) -- off by default so the suite stays well inside the driver's time limit (VERDICT r04
 # next #5); every BASELINE config still runs at full size once without it.

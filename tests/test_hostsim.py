@@ -427,7 +427,8 @@ ONESHOT = {"mesh": "0", "oneshot": str(1 << 20), "push": "0", "push2": "0"}  # F
 def _form_env(form):
     """The mesh's forms: two launches (pull), one-shot, the push reduce-scatter, and push in
     both phases (the owner's tree also stores its block into every peer)."""
-    return {"FTAR_ONESHOT_MAX": ONESHOT[form], "FTAR_PUSH": {"push": "1", "push2": "2"}.get(form, "0")}
+    return {"FTAR_ONESHOT_MAX": ONESHOT[form], "FTAR_PUSH": {"push": "1", "push2": "2"}.get(form, "0"),
+            "FTAR_MESH_WAIT": "1"}
 
 
 def _mesh_launches(p, form):
