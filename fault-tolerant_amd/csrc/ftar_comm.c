@@ -144,45 +144,76 @@ int ftar_set_kills(ftar_comm *c, const ftar_kill *kills, int nkills)
 
 /* ---- bootstrap ------------------------------------------------------------ */
 
+/* The comm's environment defaults: every value must be a whole number (or a decimal where
+ * `real`) inside [lo, hi] -- "auto", "on", "" or "1x" are refused with FTAR_ERR_ARG and a
+ * message naming the variable, never read as 0 the way atoi would.  The same
+ * ranges ftar_comm_set_option accepts. */
+struct env_knob {
+    const char *name;
+    double lo, hi, dflt;
+    int real;
+};
+
+static int env_value(int rank, const struct env_knob *k, double *out)
+{
+    const char *e = getenv(k->name);
+    *out = k->dflt;
+    if (!e) return 0;
+    char *end = NULL;
+    double v = k->real ? strtod(e, &end) : (double)strtoll(e, &end, 10);
+    if (end == e || *end != 0 || !(v >= k->lo && v <= k->hi)) {
+        fprintf(stderr, "ftar: rank %d: %s=%s is not a %s in [%g, %g]: refused\n", rank, k->name, e,
+                k->real ? "number" : "whole number", k->lo, k->hi);
+        return FTAR_ERR_ARG;
+    }
+    *out = v;
+    return 0;
+}
+
 int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int device)
 {
     *out = NULL;
     if (!job || rank < 0 || size < 1 || rank >= size || size > FTAR_MAX_RANKS) return FTAR_ERR_ARG;
-    const char *e;
     ftar_comm *c = (ftar_comm *)calloc(1, sizeof(ftar_comm));
     if (!c) return FTAR_ERR_NOMEM;
     c->wrank = rank;
     c->wsize = size;
     c->device = device;
-    c->verbose = getenv("FTAR_VERBOSE") ? atoi(getenv("FTAR_VERBOSE")) : 0;
-    c->loop_seconds = getenv("FTAR_LOOP_SECONDS") ? atof(getenv("FTAR_LOOP_SECONDS")) : 0.0;
-    c->overlap = getenv("FTAR_OVERLAP") ? atoi(getenv("FTAR_OVERLAP")) : 1;
-    c->relay = getenv("FTAR_RELAY") ? atoi(getenv("FTAR_RELAY")) : 1;
-    c->redundancy = 2;
-    if ((e = getenv("FTAR_REDUNDANCY"))) {
-        /* the same values ftar_comm_set_option accepts (it refuses others with FTAR_ERR_ARG);
-         * the whole string must be the number: "auto", "on" or "" are refused, not read as 0 */
-        char *end = NULL;
-        long v = strtol(e, &end, 10);
-        if (end == e || *end != 0 || v < 0 || v > 2) {
-            fprintf(stderr, "ftar: rank %d: FTAR_REDUNDANCY=%s is not 0, 1 or 2: refused\n", rank, e);
+    const double MiB = (double)(1 << 20), SZ = 4611686018427387904.0; /* sizes up to 2^62 */
+    const struct env_knob knobs[] = {
+        {"FTAR_VERBOSE", 0, 9, 0, 0},         {"FTAR_LOOP_SECONDS", 0, 1e6, 0, 1},
+        {"FTAR_OVERLAP", 0, 1, 1, 0},         {"FTAR_RELAY", 0, 1, 1, 0},
+        {"FTAR_REDUNDANCY", 0, 2, 2, 0},      {"FTAR_COPY_ENGINE", 0, 1, 0, 0},
+        {"FTAR_MESH", 0, 1, 1, 0},            {"FTAR_PUSH", 0, 2, 0, 0},
+        {"FTAR_MESH_WAIT", 0, 1, 1, 0},       {"FTAR_GATE", 0, 1, 1, 0},
+        {"FTAR_GATE_HOLD_US", 0, 1e12, 2000, 1}, {"FTAR_GATE_MAX", 0, SZ, MiB, 0},
+        {"FTAR_ONESHOT_MAX", 0, SZ, MiB, 0},  {"FTAR_EXPORT", 0, 1, 1, 0},
+        {"FTAR_STAGE_MAX", 0, SZ, MiB, 0},    {"FTAR_HOST_PIPE", 0, 1, 1, 0},
+        {"FTAR_RELAY_MIN", 0, SZ, 4 * MiB, 0},
+    };
+    double v[sizeof(knobs) / sizeof(knobs[0])];
+    for (size_t i = 0; i < sizeof(knobs) / sizeof(knobs[0]); i++)
+        if (env_value(rank, &knobs[i], &v[i])) {
             free(c);
             return FTAR_ERR_ARG;
         }
-        c->redundancy = (int)v;
-    }
-    c->copy_engine = getenv("FTAR_COPY_ENGINE") ? atoi(getenv("FTAR_COPY_ENGINE")) : 0;
-    c->mesh = getenv("FTAR_MESH") ? atoi(getenv("FTAR_MESH")) : 1;
-    c->push = getenv("FTAR_PUSH") ? atoi(getenv("FTAR_PUSH")) : 0;
-    c->mesh_wait = getenv("FTAR_MESH_WAIT") ? atoi(getenv("FTAR_MESH_WAIT")) != 0 : 1;
-    c->gate = getenv("FTAR_GATE") ? atoi(getenv("FTAR_GATE")) != 0 : 1;
-    c->gate_hold_s = (getenv("FTAR_GATE_HOLD_US") ? atof(getenv("FTAR_GATE_HOLD_US")) : 2000.0) * 1e-6;
-    c->gate_max = getenv("FTAR_GATE_MAX") ? (size_t)atoll(getenv("FTAR_GATE_MAX")) : ((size_t)1 << 20);
-    c->oneshot_max = getenv("FTAR_ONESHOT_MAX") ? (size_t)atoll(getenv("FTAR_ONESHOT_MAX")) : ((size_t)1 << 20);
-    c->export_user = getenv("FTAR_EXPORT") ? atoi(getenv("FTAR_EXPORT")) : 1;
-    c->stage_max = getenv("FTAR_STAGE_MAX") ? (size_t)atoll(getenv("FTAR_STAGE_MAX")) : ((size_t)1 << 20);
-    c->host_pipe = getenv("FTAR_HOST_PIPE") ? atoi(getenv("FTAR_HOST_PIPE")) : 1;
-    c->relay_min = getenv("FTAR_RELAY_MIN") ? (size_t)atoll(getenv("FTAR_RELAY_MIN")) : ((size_t)4 << 20);
+    c->verbose = (int)v[0];
+    c->loop_seconds = v[1];
+    c->overlap = (int)v[2];
+    c->relay = (int)v[3];
+    c->redundancy = (int)v[4];
+    c->copy_engine = (int)v[5];
+    c->mesh = (int)v[6];
+    c->push = (int)v[7];
+    c->mesh_wait = (int)v[8];
+    c->gate = (int)v[9];
+    c->gate_hold_s = v[10] * 1e-6;
+    c->gate_max = (size_t)v[11];
+    c->oneshot_max = (size_t)v[12];
+    c->export_user = (int)v[13];
+    c->stage_max = (size_t)v[14];
+    c->host_pipe = (int)v[15];
+    c->relay_min = (size_t)v[16];
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
     if (rc) {

@@ -55,12 +55,16 @@ def test_option_errors(solo):
     assert L.ftar_comm_get_option(h, 99, ctypes.byref(v)) == 13
 
 
-@pytest.mark.parametrize("value,want", [("3", "13"), ("-1", "13"), ("auto", "13"), ("on", "13"), ("", "13"),
-                                        ("1x", "13"), ("0", "0"), ("1", "0"), ("2", "0")])
-def test_env_redundancy_out_of_range_is_refused(hostsim, monkeypatch, value, want):
+@pytest.mark.parametrize("name,value,want", [("FTAR_REDUNDANCY", v, w) for v, w in (
+    ("3", "13"), ("-1", "13"), ("auto", "13"), ("on", "13"), ("", "13"), ("1x", "13"), ("0", "0"), ("1", "0"),
+    ("2", "0"))] + [("FTAR_MESH", "on", "13"), ("FTAR_MESH_WAIT", "2", "13"), ("FTAR_GATE_MAX", "1M", "13"),
+                    ("FTAR_GATE_MAX", "16777216", "0"), ("FTAR_LOOP_SECONDS", "1.5", "0"), ("FTAR_PUSH", "3", "13"),
+                    ("FTAR_GATE_HOLD_US", "-5", "13"), ("FTAR_RELAY_MIN", "0", "0")])
+def test_env_redundancy_out_of_range_is_refused(hostsim, monkeypatch, name, value, want):
     """FTAR_REDUNDANCY in the environment accepts what ftar_comm_set_option accepts (0, 1, 2):
     a typo such as 3 -- or a word such as 'auto', which atoi would have read as 0 and so turned
-    the step-0 copy off -- is refused with FTAR_ERR_ARG and a message."""
+    the step-0 copy off -- is refused with FTAR_ERR_ARG and a message; every
+    other numeric knob of the comm likewise (a range each, whole numbers unless decimal)."""
     import subprocess
     import sys
     code = ("import ctypes, os\n"
@@ -72,8 +76,9 @@ def test_env_redundancy_out_of_range_is_refused(hostsim, monkeypatch, value, wan
             "rc = L.ftar_init_rank(ctypes.byref(h), b'/ftar-optenv-%d' % os.getpid(), 0, 1, 0)\n"
             "print(rc)\n"
             "if rc == 0: L.ftar_finalize(h)\n")
-    env = dict(os.environ, FTAR_REDUNDANCY=value, FTAR_HOSTSIM_TAG=f"optenv{os.getpid()}")
+    env = dict(os.environ, FTAR_HOSTSIM_TAG=f"optenv{os.getpid()}")
+    env[name] = value
     cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=60)
     assert cp.stdout.strip() == want, (cp.stdout, cp.stderr)
     if want != "0":
-        assert f"FTAR_REDUNDANCY={value} " in cp.stderr and "refused" in cp.stderr
+        assert f"{name}={value} " in cp.stderr and "refused" in cp.stderr
