@@ -150,3 +150,31 @@ def test_random_kills_land_mid_exchange(hostsim, tmp_path):
         mid += sum(1 for p in post if p.startswith("mid-exchange"))
     assert total >= 4, total
     assert mid * 2 >= total, (mid, total)
+
+
+def test_compare_outcomes_classes(tmp_path):
+    """tools/compare_outcomes.py: a campaign's check_fault.py rows classified as the
+    reference's fixture rows are (recovered / abort / no death / deadlock / wrong result) and
+    tabled beside them per (schedule, N)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("compare_outcomes", os.path.join(ROOT, "tools", "compare_outcomes.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    d = tmp_path / "camp" / "n12"
+    d.mkdir(parents=True)
+    hdr = "N;DELAY;BUF SIZE;KILLED;TIME;DEADLOCK;SEGFAULT;ABORT;RIGHT RESULT\n"
+    (d / "log_single_RD.csv").write_text(hdr + "12;2.0;100;1;4.0;False;False;False;True\n"
+                                         "12;3.0;100;12;4.0;False;False;True;True\n"
+                                         "12;3.0;100;12;30.0;True;False;False;True\n")
+    (d / "log_nokill_RD.csv").write_text(hdr + "12;2.0;100;0;4.0;False;False;False;True\n"
+                                         "12;2.0;100;0;4.0;False;False;False;False\n")
+    out = tmp_path / "o.md"
+    m.main(["x", str(out), str(tmp_path / "camp")])
+    text = out.read_text()
+    assert "### rd N = 12" in text
+    rows = {l.split("|")[1].strip(): l for l in text.splitlines() if l.startswith("| ")}
+    for cls, n in (("recovered", 1), ("abort", 1), ("deadlock", 1), ("no death", 1), ("wrong result", 1)):
+        assert rows[cls].split("|")[2].strip().startswith(f"{n} ("), (cls, rows[cls])
+    # the reference's RD N = 12 rows (tests/golden/ref_fault_outcomes.csv): 50 recovered, 250 aborts
+    assert rows["recovered"].split("|")[3].strip().startswith("50 (")
+    assert rows["abort"].split("|")[3].strip().startswith("250 (")
