@@ -1124,13 +1124,6 @@ def multi(args):
                 # the allgather after a host agree round, as before the device-side wait
                 # (FTAR_OPT_MESH_WAIT=0): the node times the agree the default form leaves out
                 cands["mesh_host_ag"] = (1, 1, 0, 1, g0, 0)
-            if world > 2 and comm.get_option(ftar.OPT_GATE):
-                # the allgather's launch queued behind the tree at this size too (FTAR_OPT_GATE_MAX
-                # >= S), its gate opened by the reduce-scatter's agree: the launch latency after
-                # the barrier leaves the call's non-kernel time.  On one
-                # GPU shared by the ranks the waiting launch holds CUs the others need (DESIGN.md
-                # 6); with one rank per GPU nothing else competes -- the node decides
-                cands["mesh_gated_ag"] = (1, 1, 0, 1, max(float(S), g0), 0)
         if world >= 3 and comm.get_option(ftar.OPT_RELAY):
             cands["relay2hop"] = (0, 1, 0, 1, g0)
         cands["direct"] = (0, 0, 0, 1, g0)
@@ -1171,18 +1164,15 @@ def multi(args):
     push_opt = int(comm.get_option(ftar.OPT_PUSH))
     pushed = meshed and not oneshot and push_opt != 0
     unroll = int(comm.get_option(ftar.OPT_TREE_UNROLL)) if world in (4, 8) else 1
-    # the headline's allgather queued behind the tree (mesh_gated_ag): counted in the plain pass
-    # (the profiled pass gates nothing: kernel events would time the wait)
-    gated_ag = meshed and not oneshot and not pushed and breakdown.get("plain_gated_launches", 0) > 0
     # the allgather after a host agree round (FTAR_OPT_MESH_WAIT=0) instead of the device wait
-    host_ag = meshed and not oneshot and not pushed and not gated_ag and comm.last_stats().peer_waits == 0
+    host_ag = meshed and not oneshot and not pushed and comm.last_stats().peer_waits == 0
     transport = "mesh-oneshot" if oneshot else ("mesh-push2" if push_opt == 2 and world <= 8 else "mesh-push") \
-        if pushed else "mesh-gated-ag" if gated_ag else "mesh-host-ag" if host_ag else \
+        if pushed else "mesh-host-ag" if host_ag else \
         (f"mesh-u{unroll}" if unroll > 1 else "mesh") if meshed else "relay2hop" if relayed else "direct"
     keep = bool(comm.last_stats().step0_copy)  # the headline call moved the reference's step-0 copy
     chosen_opts = {o: comm.get_option(o) for o in opts}
-    # the headline's gate limit (S when mesh_gated_ag was chosen); every later leg runs at the
-    # library's default unless it names its own
+    # the headline's gate limit; every later leg runs at the library's default unless it names
+    # its own
     head_gate_max = comm.get_option(ftar.OPT_GATE_MAX)
     comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)
 
@@ -1246,8 +1236,6 @@ def multi(args):
                    "flight), allgather as one multi-source pull (power-of-two p, no spare; same tree)",
         "mesh-u4": "Rabenseifner, one-hop mesh, tree kernel with 4 vectors per lane and source (more remote loads in "
                    "flight), allgather as one multi-source pull (power-of-two p, no spare; same tree)",
-        "mesh-gated-ag": "Rabenseifner, one-hop mesh, the allgather's multi-source pull queued behind the tree kernel "
-                         "and opened by the reduce-scatter's agree (FTAR_OPT_GATE_MAX >= S; power-of-two p, no spare)",
         "mesh-push": "Rabenseifner, one-hop mesh, push form: every rank stores its part of each block into the "
                      "owner's HBM (p-1 remote-store copies in one launch), each owner reduces its block locally in the "
                      "same tree, allgather as one multi-source pull (power-of-two p, no spare)",
@@ -1415,10 +1403,7 @@ def multi(args):
                         ("relay2hop", (1, 1, 0, 0, 0)), ("direct", (0, 1, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)))
                        if pow2 or not name.startswith("mesh")]
             if pow2 and world > 2:
-                # the allgather queued behind the tree at the job's size (transport selection's
-                # mesh_gated_ag)
-                checks.append(("mesh_gated_ag", (1, 1, 0, 0, 1, 0, 1, 0), raben_fn, None,
-                               {ftar.OPT_GATE_MAX: max(float(S), gmax_lib)}))
+                # the allgather after the reduce-scatter's host agree (transport selection's mesh_host_ag)
                 checks.append(("mesh_host_ag", (1, 1, 0, 0, 1, 0, 1, 0), raben_fn, None, {}))
             if pow2:
                 checks += [(name, vals, raben_fn, min(16384, args.count), {}) for name, vals in
@@ -1531,7 +1516,6 @@ def multi(args):
         # the reference's step-0 full exchange.  Each variant records its own failure.
         out = {}
         variants = (("mesh", (1, 1, 0, 0, 1)), ("mesh_host_ag", (1, 1, 0, 0, 1, 0, 1, 0)),
-                    ("mesh_gated_ag", (1, 1, 0, 0, 1, 0, 1, 0)),
                     ("mesh_push", (1, 1, 0, 0, 1, 1)), ("mesh_push2", (1, 1, 0, 0, 1, 2)),
                     ("relay2hop", (1, 1, 0, 0, 0)),
                     ("direct", (0, 1, 0, 0, 0)), ("direct_serial", (0, 0, 0, 0, 0)), ("copy_engine", (0, 1, 1, 0, 0)),
@@ -1543,20 +1527,13 @@ def multi(args):
                 if time_left() < 10:
                     out[name] = {"skipped": "budget"}
                     continue
-                if name == "mesh_gated_ag" and (world == 2 or not comm.get_option(ftar.OPT_GATE)):
-                    continue
                 if name == "mesh_host_ag" and world == 2:
                     continue
                 try:
                     maybe_fail(f"transports:{name}")
                     set_opts(vals)
-                    # every variant starts from the library's gate limit: a variant that raised
-                    # with the allgather gated must not leave it on for the next rows
-                    comm.set_option(ftar.OPT_GATE_MAX, max(float(S), gmax_lib) if name == "mesh_gated_ag" else gmax_lib)
-                    try:
-                        tv, kv = timed_split(raben)
-                    finally:
-                        comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)
+                    comm.set_option(ftar.OPT_GATE_MAX, gmax_lib)  # every variant at the library's gate limit
+                    tv, kv = timed_split(raben)
                     lb = timed.link_bytes
                     tv_rd = timed(rd)[0] if name in ("relay2hop", "direct", "copy_engine") else None
                     bd = timed_split.breakdown
@@ -1571,9 +1548,6 @@ def multi(args):
                                  "peer_waits": bd.get("peer_waits")}
                     if tv_rd:
                         out[name].update({"rd_ms": round(tv_rd * 1e3, 4), "rd_algbw_GBps": round(S / tv_rd / 1e9, 2)})
-                    if name == "mesh_gated_ag":
-                        out[name]["plain_gated_launches"] = timed_split.breakdown.get("plain_gated_launches")
-                        out[name]["plain_gate_holds"] = timed_split.breakdown.get("plain_gate_holds")
                 except Exception as e:
                     out[name] = {"error": str(e)[-300:]}
         finally:
@@ -1609,10 +1583,9 @@ def multi(args):
                 for name, fn, extra in (("raben", comm.allreduce_rabenseifner, None),
                                         ("raben_no_oneshot", comm.allreduce_rabenseifner, {ftar.OPT_ONESHOT_MAX: 0}),
                                         ("rd", comm.recursive_doubling, None),
-                                        # mid-size calls with their predictable launches queued
-                                        # behind relayed gates (off by default: DESIGN.md 6)
-                                        ("raben_midgate", comm.allreduce_rabenseifner,
-                                         {ftar.OPT_GATE_MAX: MID_GATE_MAX}),
+                                        # mid-size RD calls with steps 1.. queued behind relayed
+                                        # gates (off by default: DESIGN.md 6; the mesh's allgather
+                                        # is ordered on the device instead)
                                         ("rd_midgate", comm.recursive_doubling, {ftar.OPT_GATE_MAX: MID_GATE_MAX})):
                     if name == "raben_no_oneshot" and (not (pow2 and comm.get_option(ftar.OPT_MESH) and oneshot_max > 0)
                                                        or (world > 2 and 4 * n > oneshot_max)):

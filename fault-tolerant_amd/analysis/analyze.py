@@ -260,9 +260,6 @@ def decisions(line: dict) -> dict:
         "transport_ms": times,
         "transport_inexact_or_failed": sorted(set(sel.get("inexact") or []) | set(sel.get("failed") or {})),
         "never_fastest": sorted(k for k in times if k != sel.get("chosen")),
-        # the allgather queued behind the tree at the headline size
-        "gated_ag_faster": (times["mesh_gated_ag"] < times["mesh"]) if "mesh_gated_ag" in times and "mesh" in times
-        else None,
         # the allgather ordered on the device (the default) vs after a host agree (FTAR_OPT_MESH_WAIT=0)
         "device_wait_faster": (times["mesh"] < times["mesh_host_ag"]) if "mesh_host_ag" in times and "mesh" in times
         else None,

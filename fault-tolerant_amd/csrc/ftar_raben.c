@@ -619,10 +619,10 @@ static int rb_mesh(rb_ctx *x, const void *sbuf, void *rbuf)
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
     if (x->devwait) return rb_mesh_devwait(x, rbuf, lb0);
-    /* up to FTAR_GATE_MAX: the allgather's launch queued right behind the tree, its gate
-     * opened where it would otherwise be launched (after the reduce-scatter's agree) */
-    ns = rb_mesh_ag_segs(x, rbuf, segs);
-    if (c->gate && x->count * x->es <= c->gate_max) ftar_prelaunch(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP, NULL, NULL, 0);
+    /* FTAR_OPT_MESH_WAIT=0: the allgather launched after the reduce-scatter's agree round.
+     * (Round 4's form with the allgather queued behind the tree behind a host-opened gate,
+     * FTAR_GATE_MAX >= S, was slower in every rehearsal and is superseded by the device wait:
+     * removed in round 6.) */
     ftar_launched(c, FTAR_PH_LOOP, 0); /* every step's DURING point: the one launch is in flight */
     for (int s = 1; s < L; s++) ftar_maybe_die(c, FTAR_PH_LOOP, s, FTAR_PT_DURING);
     ftar_drain(c);
@@ -640,8 +640,7 @@ allgather:
     for (int s = L - 1; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_BEFORE);
     ftar_enter(c);
     ns = rb_mesh_ag_segs(x, rbuf, segs);
-    if (c->gplan.valid || fdev_gate_pending(c->dev)) ftar_run_gated_or(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
-    else ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
+    ftar_run(c, x->dtype, x->op, segs, ns, FDEV_TAG_STEP);
     ftar_launched(c, FTAR_PH_AG, L - 1);
     for (int s = L - 2; s >= 0; s--) ftar_maybe_die(c, FTAR_PH_AG, s, FTAR_PT_DURING);
     ftar_drain(c);

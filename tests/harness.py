@@ -79,9 +79,6 @@ def wide(*cases):
     """Parametrize values that run only under FTAR_GPU_WIDE=1."""
     return list(cases) if WIDE else []
 GATES_ON = {"FTAR_GATE": "1", "FTAR_FLAG_SYNC": "1"}
-# the mesh's allgather after the reduce-scatter's host agree (not ordered on the device): the
-# form whose allgather launch a gate can queue behind the tree (FTAR_GATE_MAX >= S)
-HOST_AG = {"FTAR_MESH_WAIT": "0"}
 
 
 def run_probe(algo: str, inputs, kills=(), op: int = 0, iters: int = 1, backend: str = "hostsim",

@@ -418,22 +418,22 @@ def test_bench_multi_watchdog_prints_and_exits(hostsim, tmp_path):
 
 
 @pytest.mark.timeout(240)
-def test_bench_multi_four_ranks_gated_allgather(hostsim, tmp_path):
-    """Four ranks, 4 MiB per rank (above the one-shot and gate limits): the transport
-    selection times `mesh_gated_ag` -- the mesh with its allgather queued behind the tree
-    (FTAR_OPT_GATE_MAX >= S) -- beside the others, exact_on_node checks it at the job's size,
-    the transports leg reports its gated launches, node_decisions says whether it was faster,
-    and configs[2]'s roofline block carries L = 2 steps of the reference's movement."""
+def test_bench_multi_four_ranks_device_wait(hostsim, tmp_path):
+    """Four ranks, 4 MiB per rank (above the one-shot and gate limits): the default mesh orders
+    its allgather behind the peers' trees on the device (the transports leg counts its peer
+    waits); the transport selection times `mesh_host_ag` -- the allgather after a host agree
+    round -- beside the others, exact_on_node checks it at the job's size, node_decisions says
+    whether the device wait was faster, and configs[2]'s roofline block carries L = 2 steps of
+    the reference's movement."""
     cp, lines, took = _torchrun_cpu(tmp_path, {}, ["--side-budget", "5", "--no-c5", "--no-xgmi", "--no-cpu-baseline"],
                                     200, nproc=4, count=1 << 20)
     assert cp.returncode == 0, cp.stderr[-3000:]
     fin = lines[-1]
     sel = fin["transport_selection"]
-    assert "mesh_gated_ag_ms" in sel and "mesh_ms" in sel and not sel["inexact"] and not sel["failed"], sel
-    assert fin["exact_on_node"]["mesh_gated_ag"] and fin["exact_on_node"]["all_exact"], fin["exact_on_node"]
-    assert fin["transports"]["mesh_gated_ag"]["plain_gated_launches"] > 0, fin["transports"]["mesh_gated_ag"]
+    assert "mesh_ms" in sel and not sel["inexact"] and not sel["failed"], sel
+    assert fin["exact_on_node"]["all_exact"], fin["exact_on_node"]
+    assert fin["transports"]["mesh"]["peer_waits"] > 0, fin["transports"]["mesh"]
     nd = fin["node_decisions"]
-    assert nd["gated_ag_faster"] in (True, False), nd
     # the device-ordered allgather (default) against the host-agree form: timed, exact, decided
     assert "mesh_host_ag_ms" in sel and fin["exact_on_node"]["mesh_host_ag"], (sel, fin["exact_on_node"])
     assert nd["device_wait_faster"] in (True, False), nd

@@ -61,7 +61,7 @@ BASE = [
     (5, "raben", MIB, {"FTAR_KILL": "4:2:0:3:1"}),         # last AG step, DURING
     (5, "rd", 16384, {"FTAR_KILL": "1:1:1:3:1"}),          # RD step 1, DURING
     (4, "raben", 64 * MIB, {}),                            # 256 MiB mesh
-    (4, "raben", 64 * MIB, {"FTAR_GATE_MAX": str(256 * MIB), "FTAR_MESH_WAIT": "0"}),  # mesh_gated_ag, headline size
+    (4, "raben", 64 * MIB, {"FTAR_MESH_WAIT": "0"}),       # the headline size, allgather after a host agree
 ]
 WIDE = [
     (8, "raben", 1, {}), (8, "raben", 16384, {}), (8, "raben", 262140, {}), (8, "raben", 262148, {}),
