@@ -78,7 +78,7 @@ def test_mid_size_gates(oracle, algo, p, count):
 
 @pytest.mark.timeout(180)
 @pytest.mark.parametrize("algo,p,count", [("raben", 4, 1031), ("rd", 4, 1031), ("rd", 2, 1031),
-                                          ("rd", 4, (1 << 19) + 3), ("raben", 4, (1 << 19) + 3)])
+                                          ("rd", 4, (1 << 19) + 3)])
 def test_late_peer_device_gate_timeout_relaunches(oracle, algo, p, count):
     r = _run(oracle, algo, p, {"FTAR_GATE_HOLD_US": "0", "FTAR_GATE_TIMEOUT_MS": "30",
                                "FTAR_ONESHOT_MAX": "0" if count > 4096 else str(1 << 20)}, count=count)
