@@ -834,9 +834,11 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
                  (c->size == 2 || count * (size_t)x->es <= c->oneshot_max);
     /* push 2 (both phases) needs every peer as an extra destination of one tree: p <= 8 */
     x->push = (x->mesh && !x->oneshot && c->push) ? (c->push == 2 && c->size <= 8 ? 2 : 1) : 0;
-    /* uniform too; every block non-empty (count >= p: the allgather launch always exists) */
+    /* uniform too; every block non-empty (count >= p: the allgather launch always exists); not
+     * with FTAR_OPT_FLAG_SYNC off, the conservative mode of fenced-marker drains only (whose
+     * pinned flag words the wait also uses) */
     x->devwait = x->mesh && !x->oneshot && !x->push && c->mesh_wait && count >= (size_t)c->size &&
-                 c->size - 1 <= FDEV_MAX_PEERS;
+                 c->size - 1 <= FDEV_MAX_PEERS && fdev_get_knob(c->dev, FDEV_KNOB_FLAG_SYNC) == 1;
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);

@@ -474,6 +474,14 @@ def test_mesh_peer_wait_timeout_fallback(hostsim, oracle, p, late):
     assert all(r.status[w][0][7] == ref.status[w][0][7] + 1 for w in r.status)  # the extra round, uniform
 
 
+def test_mesh_peer_wait_off_with_flag_sync_off(hostsim, oracle):
+    """FTAR_FLAG_SYNC=0 (fenced-marker drains only, the conservative mode exact_on_node falls
+    back to) also keeps the mesh's allgather after a host agree: no peer wait, same bits."""
+    ins = oracle.random_inputs(4, 40003, seed=66)
+    o, r = _cmp(oracle.rabenseifner, "raben", ins, env=dict(_form_env("mesh"), FTAR_FLAG_SYNC="0"))
+    assert all(st[0][15] == 0 for st in r.status.values()), r.status
+
+
 @pytest.mark.parametrize("kill", [(2, 1, 0, 0), (1, 1, 1, 3), (3, 1, 0, 3), (0, 2, 1, 0), (2, 2, 0, 3), (1, 1, 0, 1)])
 def test_mesh_peer_wait_kills_abort(hostsim, oracle, kill):
     """Kills around the device wait at p = 4 (no idle rank: every failure aborts, as the
