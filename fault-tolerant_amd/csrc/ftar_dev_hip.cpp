@@ -23,17 +23,40 @@ namespace {
 char g_err[512];
 int g_reduce_variant = 1; // LDS-DMA staged (equal or faster than 0 in every C2 run)
 
-// Non-temporal 16-byte stores in every streaming kernel (FTAR_NT_STORE=0 turns them
-// off): see ftar_kernels.hip, measured on rotating buffers in profiles/r02.
-unsigned nt_store()
+// A numeric FTAR_* knob of the device layer: the whole string must be a whole number in
+// [lo, hi]; anything else is refused with g_err naming it (atoi would read "off" or "2k" as
+// 0 or 2 without a word).
+bool env_knob(const char *name, long long lo, long long hi, long long dflt, long long *out)
 {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("FTAR_NT_STORE");
-        v = e ? (atoi(e) != 0) : 1;
+    const char *e = getenv(name);
+    *out = dflt;
+    if (!e) return true;
+    char *end = nullptr;
+    long long v = strtoll(e, &end, 10);
+    if (end == e || *end != 0 || v < lo || v > hi) {
+        snprintf(g_err, sizeof(g_err), "%s=%s is not a whole number in [%lld, %lld]: refused", name, e, lo, hi);
+        return false;
     }
-    return (unsigned)v;
+    *out = v;
+    return true;
 }
+
+// The process-wide streaming knobs, read once: FTAR_NT_STORE (non-temporal 16-byte stores in
+// every streaming kernel, default 1: see ftar_kernels.hip, measured on rotating buffers in
+// profiles/r02) and FTAR_BLOCKS_PER_CU (grid cap, below).  -1: a value was refused.
+long long g_nt = -1, g_bpc = -1;
+int g_knobs = 0; // 0 unread, 1 valid, -1 refused
+
+int process_knobs()
+{
+    if (g_knobs == 0)
+        g_knobs = env_knob("FTAR_NT_STORE", 0, 1, 1, &g_nt) && env_knob("FTAR_BLOCKS_PER_CU", 1, 4096, 1024, &g_bpc)
+                      ? 1
+                      : -1;
+    return g_knobs == 1 ? 0 : 13;
+}
+
+unsigned nt_store() { return g_nt == 0 ? 0u : 1u; }
 
 int set_err(hipError_t e, const char *what)
 {
@@ -62,12 +85,7 @@ size_t esize_of(int dtype)
 // (1024/CU = 262144 workgroups) never binds below 2 GiB per operand: every 8 KiB tile
 // gets its own short-lived workgroup, the fastest mapping of the C2 sweep
 // (tools/reduce_sweep.hip, profiles/).
-unsigned blocks_per_cu()
-{
-    const char *e = getenv("FTAR_BLOCKS_PER_CU");
-    int v = e ? atoi(e) : 1024;
-    return (unsigned)(v < 1 ? 1 : v > 4096 ? 4096 : v);
-}
+unsigned blocks_per_cu() { return g_bpc > 0 ? (unsigned)g_bpc : 1024u; }
 
 struct Pending {
     hipEvent_t start, stop;
@@ -207,6 +225,17 @@ int fdev_open(int device, ftar_dev **out)
         snprintf(g_err, sizeof(g_err), "device %d out of range (%d visible)", device, ndev);
         return 101;
     }
+    // every knob checked before anything is allocated: a refused value fails the open cleanly
+    long long k_sync, k_max, k_unroll, k_ms, k_relay, k_big;
+    if (process_knobs() || !env_knob("FTAR_FLAG_SYNC", 0, 1, 1, &k_sync) ||
+        !env_knob("FTAR_FLAG_MAX_BLOCKS", 1, 1 << 20, 64, &k_max) || !env_knob("FTAR_TREE_UNROLL", 1, 4, 1, &k_unroll) ||
+        !env_knob("FTAR_GATE_TIMEOUT_MS", 1, 1ll << 40, 60000, &k_ms) ||
+        !env_knob("FTAR_GATE_RELAY_MIN", 1, 1 << 20, 2, &k_relay) || !env_knob("FTAR_GATE_BIG_BLOCKS", 0, 1 << 20, 0, &k_big))
+        return 13;
+    if (k_unroll == 3) {
+        snprintf(g_err, sizeof(g_err), "FTAR_TREE_UNROLL=3 is not 1, 2 or 4: refused");
+        return 13;
+    }
     HIPCHK(hipSetDevice(device));
     ftar_dev *d = new ftar_dev();
     d->device = device;
@@ -225,9 +254,8 @@ int fdev_open(int device, ftar_dev **out)
     HIPCHK(hipEventCreateWithFlags(&d->fence_main, hipEventDisableTiming));
     d->fence_bg = nullptr;
     {
-        const char *fs = getenv("FTAR_FLAG_SYNC"), *fm = getenv("FTAR_FLAG_MAX_BLOCKS");
-        d->flag_sync = fs ? atoi(fs) != 0 : 1;
-        d->flag_max = fm ? (unsigned)atoi(fm) : 64;
+        d->flag_sync = (int)k_sync;
+        d->flag_max = (unsigned)k_max;
         d->sig_cnt = nullptr;
         d->sig_flag = nullptr;
         d->sig_tag = 0;
@@ -238,11 +266,7 @@ int fdev_open(int device, ftar_dev **out)
         d->pre_gate_tag = 0;
         d->gate_relaunches = 0;
         d->gp[0].valid = d->gp[1].valid = 0;
-        {
-            const char *tu = getenv("FTAR_TREE_UNROLL");
-            int u = tu ? atoi(tu) : 1;
-            d->tree_unroll = (u == 2 || u == 4) ? (unsigned)u : 1u;
-        }
+        d->tree_unroll = (unsigned)k_unroll;
         int khz = 0; // wall clock of the kernels (s_memrealtime), 100 MHz on CDNA
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
             (void)hipGetLastError();
@@ -251,10 +275,7 @@ int fdev_open(int device, ftar_dev **out)
         // FTAR_GATE_TIMEOUT_MS (default 60 s): a gate still closed this long is given up by
         // the device (the workgroups return untouched) and the launch is relaunched ungated at
         // the next drain; the host normally gives a gate up far sooner (FTAR_GATE_HOLD_US)
-        const char *gt = getenv("FTAR_GATE_TIMEOUT_MS");
-        long long ms = gt ? atoll(gt) : 60000;
-        if (ms < 1) ms = 1;
-        d->gate_ticks = (unsigned long long)khz * (unsigned long long)ms;
+        d->gate_ticks = (unsigned long long)khz * (unsigned long long)k_ms;
         if (d->flag_sync) {
             HIPCHK(hipMalloc((void **)&d->sig_cnt, 256));
             HIPCHK(hipMemset(d->sig_cnt, 0, 256));
@@ -276,14 +297,9 @@ int fdev_open(int device, ftar_dev **out)
         d->fence_pre = nullptr;
         d->gate_dw = nullptr;
         d->big_pending = 0;
-        {
-            const char *bb = getenv("FTAR_GATE_BIG_BLOCKS");
-            long v = bb ? atol(bb) : (long)prop.multiProcessorCount / 2;
-            d->big_blocks = (unsigned)(v < 1 ? 1 : v);
-            const char *rm = getenv("FTAR_GATE_RELAY_MIN");
-            long r = rm ? atol(rm) : 2;
-            d->relay_min = (unsigned)(r < 1 ? 1 : r);
-        }
+        // FTAR_GATE_BIG_BLOCKS unset (0): half the CUs
+        d->big_blocks = k_big > 0 ? (unsigned)k_big : (unsigned)(prop.multiProcessorCount / 2 > 0 ? prop.multiProcessorCount / 2 : 1);
+        d->relay_min = (unsigned)k_relay;
         if (d->flag_sync) {
             HIPCHK(hipEventCreateWithFlags(&d->fence_pre, hipEventDisableTiming)); // fenced, see sync_stream
             HIPCHK(hipMalloc((void **)&d->gate_dw, 256));
@@ -1677,6 +1693,7 @@ int fdev_reduce_local(const void *in, void *inout, size_t n, int dtype, int op, 
         return 13;
     }
     if (n == 0) return 0;
+    if (process_knobs()) return 13; // FTAR_NT_STORE / FTAR_BLOCKS_PER_CU refused (g_err names it)
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     if (n > SIZE_MAX / es || check_local_ptr(in, n * es, dev) || check_local_ptr(inout, n * es, dev)) {

@@ -623,3 +623,15 @@ def test_float_sum_within_stated_tolerance(oracle, algo, p):
     for w in range(p):
         err = np.abs(r.outputs[w][0].astype(np.float64) - exact)
         assert (err <= bound).all(), (w, float((err / np.maximum(bound, 1e-300)).max()))
+
+
+@pytest.mark.parametrize("name,value", [("FTAR_FLAG_MAX_BLOCKS", "lots"), ("FTAR_TREE_UNROLL", "3"),
+                                        ("FTAR_NT_STORE", "off"), ("FTAR_GATE_TIMEOUT_MS", "0")])
+def test_device_knob_refused(oracle, name, value):
+    """A device-layer knob that is not a whole number in its range is refused when the rank
+    opens its device (the job fails with one line naming it), never read as 0 the way atoi
+    would read it."""
+    ins = oracle.random_inputs(2, 1031, seed=5)
+    r = H.run_probe("raben", ins, backend="gpu", devmap=ALL_ON_GPU0, timeout=120, env_extra={name: value})
+    assert r.returncode != 0 and not r.outputs
+    assert f"{name}={value} is not a" in r.stderr and "refused" in r.stderr, r.stderr[-1500:]
