@@ -3,7 +3,7 @@
  *
  * One ftar_dev per rank process: the HIP device it drives, one non-blocking stream
  * the schedules enqueue on, exportable (IPC) allocations, and the segment kernel.
- * Implemented in ftar_dev_hip.cpp + ftar_kernels.hip.  The schedules never see a HIP
+ * Implemented in ftar_dev_{hip,launch,gate,trace}.cpp + ftar_kernels.hip.  The schedules never see a HIP
  * type: everything crosses this header as plain pointers and sizes.
  */
 #ifndef FTAR_DEV_H

@@ -4,7 +4,7 @@ TEST INFRASTRUCTURE.  On one GPU every rank's "peer" memory is the same HBM behi
 L2s, so a missing write-back or invalidate can never show up as a wrong result there
 (VERDICT r04 weak #1).  What can be checked without the node is the DISCIPLINE the node's
 visibility rests on: every launch, drain, fenced marker, gate verdict and barrier of every
-rank is logged (fault-tolerant_amd/csrc/ftar_dev_hip.cpp, `tr_launch`; the barrier lines
+rank is logged (fault-tolerant_amd/csrc/ftar_dev_trace.cpp, `tr_launch`; the barrier lines
 from ftar_sync) and this module verifies two rules over all ranks' logs:
 
 * release -- a read by rank Y of buffer B (owner:name, byte range) that runs after Y passed
