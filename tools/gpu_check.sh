@@ -10,7 +10,7 @@
 #   prof       rocprofv3 kernel trace + stats of bench.py N = 1
 #   pmc        one rocprofv3 --pmc pass per counter (FETCH_SIZE, WRITE_SIZE) of bench.py
 #   hbmsweep   tools/hbm_sweep.hip: C2 variants and calibration streams, rotating buffers
-#   ipcprobe   tools/ipc_probe.hip: IPC export after free / regrowth
+#   ipcprobe   tools/ipc_probe.hip: IPC export after free / regrowth, import capacity (N = 32 / 64)
 #   rehearse   bench.py's N > 1 line with 2 / 4 ranks on GPU 0 (gloo), every leg
 #   rehearse8  the same with 8 ranks (the driver's N = 8 path on one device)
 #   meshprof   rank 0 of a 4 / 8-rank mesh job under rocprofv3 (trace, FETCH_SIZE, WRITE_SIZE)
@@ -70,6 +70,9 @@ fi
 if has ipcprobe; then
   timeout -k 10 120 tools/_build/ipc_probe > "$OUT/ipc_probe.json" 2>&1
   rc=$?; cat "$OUT/ipc_probe.json"; stop_on_fault $rc ipcprobe
+  # the capacity phase again with 128 MiB blocks: 252 imports mapping 31.5 GiB of the peer's HBM
+  timeout -k 10 180 tools/_build/ipc_probe 252 128 > "$OUT/ipc_probe_128.json" 2>&1
+  rc=$?; grep capacity "$OUT/ipc_probe_128.json"; stop_on_fault $rc ipcprobe_128
 fi
 if has rehearse || has rehearse8; then
   ns="2 4"; has rehearse8 && ns="8"

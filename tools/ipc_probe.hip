@@ -9,6 +9,13 @@
 //   growth: the library's workspace pattern -- both processes allocate 4 blocks, export,
 //       import the peer's 4, close them, free their own, grow x2, for 2 MiB .. 1 GiB --
 //       counting exports refused on the first try, with the overlap test.
+//   capacity: the per-process IPC resources of the reference's largest NP (4
+//       exported buffers x 31 peers = 124 imports per rank at N = 32, 252 at N = 64, which one
+//       GPU cannot host as 32 / 64 processes): each process exports K blocks (a distinct
+//       pattern in each), imports the peer's K, checks every import reads its owner's pattern,
+//       stores a word into every imported block, and each owner checks the words landed;
+//       import / close times reported at 124 and at K.
+// Usage: ipc_probe [K blocks per process, default 252] [MiB per block, default 4]
 // Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/ipc_probe.hip -o tools/_build/ipc_probe
 #include <hip/hip_runtime.h>
 #include <stdatomic.h>
@@ -18,14 +25,17 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/wait.h>
+#include <time.h>
 #include <unistd.h>
 
 #define NB 4
 #define MAXR 16
+#define MAXK 256
 
 struct Shm {
     _Atomic int bar[2];
     hipIpcMemHandle_t h[2][NB];
+    hipIpcMemHandle_t hk[2][MAXK];
     int fail;
 };
 
@@ -142,8 +152,93 @@ static void growth()
     fflush(stdout);
 }
 
-int main()
+static double now_ms()
 {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+
+static unsigned pattern(int owner, int b) { return 0x51000000u + (unsigned)owner * 0x10000u + (unsigned)b; }
+
+static void capacity(int K, size_t s)
+{
+    static void *own[MAXK], *imp[MAXK];
+    int alloc_ok = 0, export_ok = 0, import_ok = 0, read_ok = 0, write_ok = 0, landed_ok = 0;
+    for (int b = 0; b < K; b++) {
+        own[b] = nullptr;
+        if (hipMalloc(&own[b], s) != hipSuccess) {
+            (void)hipGetLastError();
+            own[b] = nullptr;
+            continue;
+        }
+        alloc_ok++;
+        (void)hipMemsetD32((hipDeviceptr_t)own[b], pattern(me, b), s / 4);
+        if (hipIpcGetMemHandle(&S->hk[me][b], own[b]) == hipSuccess) export_ok++;
+        else (void)hipGetLastError();
+    }
+    (void)hipDeviceSynchronize();
+    barrier();
+    double t0 = now_ms(), t124 = 0;
+    for (int b = 0; b < K; b++) {
+        imp[b] = nullptr;
+        if (hipIpcOpenMemHandle(&imp[b], S->hk[1 - me][b], hipIpcMemLazyEnablePeerAccess) == hipSuccess) import_ok++;
+        else {
+            (void)hipGetLastError();
+            imp[b] = nullptr;
+        }
+        if (b + 1 == 124) t124 = now_ms() - t0;
+    }
+    const double t_import = now_ms() - t0;
+    for (int b = 0; b < K; b++) {
+        if (!imp[b]) continue;
+        unsigned head[4] = {}, tail[4] = {};
+        if (hipMemcpy(head, imp[b], 16, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(tail, (char *)imp[b] + s - 16, 16, hipMemcpyDeviceToHost) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        bool ok = true;
+        for (int i = 0; i < 4; i++) ok = ok && head[i] == pattern(1 - me, b) && tail[i] == pattern(1 - me, b);
+        read_ok += ok;
+        const unsigned mark = 0xABC00000u + (unsigned)me * 0x1000u + (unsigned)b;
+        if (hipMemcpy((char *)imp[b] + 64, &mark, 4, hipMemcpyHostToDevice) == hipSuccess) write_ok++;
+        else (void)hipGetLastError();
+    }
+    (void)hipDeviceSynchronize();
+    barrier();
+    for (int b = 0; b < K; b++) {
+        unsigned w = 0;
+        if (own[b] && hipMemcpy(&w, (char *)own[b] + 64, 4, hipMemcpyDeviceToHost) == hipSuccess)
+            landed_ok += w == 0xABC00000u + (unsigned)(1 - me) * 0x1000u + (unsigned)b;
+    }
+    barrier();
+    t0 = now_ms();
+    for (int b = 0; b < K; b++)
+        if (imp[b]) (void)hipIpcCloseMemHandle(imp[b]);
+    const double t_close = now_ms() - t0;
+    barrier();
+    for (int b = 0; b < K; b++)
+        if (own[b]) (void)hipFree(own[b]);
+    const bool all = alloc_ok == K && export_ok == K && import_ok == K && read_ok == K && write_ok == K && landed_ok == K;
+    if (!all) S->fail = 1;
+    printf("{\"phase\": \"capacity\", \"rank\": %d, \"blocks\": %d, \"MiB_per_block\": %zu, \"mapped_GiB\": %.2f, "
+           "\"alloc_ok\": %d, \"export_ok\": %d, \"import_ok\": %d, \"read_ok\": %d, \"write_ok\": %d, "
+           "\"landed_ok\": %d, \"all_ok\": %s, \"import_ms_first_124\": %.2f, \"import_ms_all\": %.2f, "
+           "\"close_ms_all\": %.2f}\n",
+           me, K, s >> 20, (double)K * (double)s / (1u << 30), alloc_ok, export_ok, import_ok, read_ok, write_ok,
+           landed_ok, all ? "true" : "false", t124, t_import, t_close);
+    fflush(stdout);
+}
+
+int main(int argc, char **argv)
+{
+    int K = argc > 1 ? atoi(argv[1]) : 252;
+    size_t mib = argc > 2 ? (size_t)atoll(argv[2]) : 4;
+    if (K < 1 || K > MAXK || mib < 1 || mib > 1024) {
+        fprintf(stderr, "usage: ipc_probe [K 1..%d] [MiB 1..1024]\n", MAXK);
+        return 2;
+    }
     S = (Shm *)mmap(nullptr, sizeof(Shm), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     memset(S, 0, sizeof(Shm));
     pid_t kids[2];
@@ -154,6 +249,7 @@ int main()
             if (hipSetDevice(0) != hipSuccess) _exit(3);
             importer_reuse();
             growth();
+            capacity(K, mib << 20);
             _exit(0);
         }
     }
