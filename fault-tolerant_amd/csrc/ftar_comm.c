@@ -214,6 +214,11 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->stage_max = (size_t)v[14];
     c->host_pipe = (int)v[15];
     c->relay_min = (size_t)v[16];
+    c->ucache_idle = FTAR_UCACHE_IDLE;
+#ifdef FTAR_TEST_HOOKS
+    /* TEST-ONLY: a short idle limit, so a test reaches the send-buffer caches' evictions */
+    if (getenv("FTAR_UCACHE_IDLE_CALLS")) c->ucache_idle = (uint64_t)atoll(getenv("FTAR_UCACHE_IDLE_CALLS"));
+#endif
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
     if (rc) {
@@ -300,16 +305,52 @@ static void release_peers(ftar_comm *c)
             }
 }
 
+static void drop_mapping(ftar_comm *c, int w, int k)
+{
+    if (c->ucache[w][k].base) {
+        fdev_trace_unregion(c->dev, c->ucache[w][k].base);
+        fdev_unimport(c->dev, c->ucache[w][k].base);
+    }
+    c->ucache[w][k].base = NULL;
+    c->ucache[w][k].id = 0;
+}
+
 static void release_user_peers(ftar_comm *c)
 {
     for (int w = 0; w < c->wsize; w++)
-        for (int k = 0; k < FTAR_UCACHE; k++)
-            if (c->ucache[w][k].base) {
-                fdev_trace_unregion(c->dev, c->ucache[w][k].base);
-                fdev_unimport(c->dev, c->ucache[w][k].base);
-                c->ucache[w][k].base = NULL;
-                c->ucache[w][k].id = 0;
-            }
+        for (int k = 0; k < FTAR_UCACHE; k++) drop_mapping(c, w, k);
+}
+
+/* The exporter's side of the send-buffer caches (ftar_internal.h): entries idle for
+ * FTAR_UCACHE_IDLE calls leave first, then this call's allocation is a hit (1), enters a
+ * free entry (1, *fresh: the peers map it now), or finds the cache full (0: staged).  The
+ * peers' peer_sbuf applies the same rule to the same sequence of ids, so its cache of this
+ * rank holds exactly these ids. */
+static int xcache_admit(ftar_comm *c, uint64_t id, int *fresh)
+{
+    const uint64_t now = (uint64_t)c->ncalls;
+    *fresh = 0;
+    for (int k = 0; k < FTAR_UCACHE; k++)
+        if (c->xcache[k].id && c->xcache[k].last + c->ucache_idle < now) c->xcache[k].id = 0;
+    int free_k = -1;
+    for (int k = 0; k < FTAR_UCACHE; k++) {
+        if (c->xcache[k].id == id) {
+            c->xcache[k].last = now;
+            return 1;
+        }
+        if (!c->xcache[k].id && free_k < 0) free_k = k;
+    }
+    if (free_k < 0) return 0;
+    c->xcache[free_k].id = id;
+    c->xcache[free_k].last = now;
+    *fresh = 1;
+    return 1;
+}
+
+static void xcache_forget(ftar_comm *c, uint64_t id)
+{
+    for (int k = 0; k < FTAR_UCACHE; k++)
+        if (c->xcache[k].id == id) c->xcache[k].id = 0;
 }
 
 int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
@@ -317,13 +358,21 @@ int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
     ftar_slot *me = &c->job.shm->slot[c->wrank];
     uint64_t id = 0;
     size_t off = 0;
+    int fresh = 0;
     ftar_inputs_done(c);
     /* a small input is cheaper staged than read in place: the staging copy signals its own
      * completion, where peers reading the caller's memory need a fenced marker */
     if (bytes <= c->stage_max) alias_ok = 0;
-    int ok = alias_ok && c->export_user && bytes && fdev_export_range(c->dev, sbuf, bytes, me->uhandle, &id, &off) == 0;
+    int ok = alias_ok && c->export_user && bytes && fdev_export_range(c->dev, sbuf, bytes, NULL, &id, &off) == 0 &&
+             xcache_admit(c, id, &fresh);
+    /* a new entry: export its handle now (the peers map it after the call's first barrier) */
+    if (ok && fresh && fdev_export_range(c->dev, sbuf, bytes, me->uhandle, &id, &off) != 0) {
+        xcache_forget(c, id);
+        ok = 0;
+    }
     me->uid = ok ? id : 0;
     me->uoff = off;
+    me->unew = ok && fresh;
     me->useq = (uint64_t)c->ncalls; /* a rank that dies before this point leaves an older tag */
     if (ok) {
         char nm[32];
@@ -336,64 +385,84 @@ int ftar_stage_input(ftar_comm *c, const void *sbuf, size_t bytes, int alias_ok)
         fdev_fence_next_drain(c->dev);
     }
     c->in_bytes = bytes;
-    if (c->verbose >= 2) fprintf(stderr, "ftar[%d] call %d: input %s\n", c->wrank, c->ncalls, ok ? "in place" : "staged");
+    if (c->verbose >= 2)
+        fprintf(stderr, "ftar[%d] call %d: input %s (allocation %llu, offset %zu%s)\n", c->wrank, c->ncalls,
+                ok ? "in place" : "staged", (unsigned long long)me->uid, (size_t)me->uoff, fresh ? ", new" : "");
     return ok;
 }
 
+/* Rank w's exported send buffer as this rank maps it: the importer's side of xcache_admit. */
 static void *peer_sbuf(ftar_comm *c, int w, int *failed)
 {
     ftar_slot *s = &c->job.shm->slot[w];
-    uint64_t id = s->uid;
-    if (s->useq != (uint64_t)c->ncalls || !id) return NULL; /* staged in IN, or not published (dead) */
-    int victim = 0;
-    for (int k = 0; k < FTAR_UCACHE; k++) {
-        if (c->ucache[w][k].base && c->ucache[w][k].id == id) {
-            c->ucache[w][k].used = ++c->ucache_clock;
+    const uint64_t id = s->uid, now = (uint64_t)c->ncalls;
+    if (s->useq != now || !id) return NULL; /* staged in IN, or not published (dead) */
+    for (int k = 0; k < FTAR_UCACHE; k++)
+        if (c->ucache[w][k].base && c->ucache[w][k].last + c->ucache_idle < now) drop_mapping(c, w, k);
+    int k = -1;
+    for (int j = 0; j < FTAR_UCACHE; j++) {
+        if (c->ucache[w][j].base && c->ucache[w][j].id == id) {
+            c->ucache[w][j].last = now;
             char nm[32];
             snprintf(nm, sizeof(nm), "U%llu", (unsigned long long)id);
-            fdev_trace_region(c->dev, c->ucache[w][k].base, s->uoff + c->in_bytes, w, nm);
-            return (char *)c->ucache[w][k].base + s->uoff;
+            fdev_trace_region(c->dev, c->ucache[w][j].base, s->uoff + c->in_bytes, w, nm);
+            return (char *)c->ucache[w][j].base + s->uoff;
         }
-        if (c->ucache[w][k].used < c->ucache[w][victim].used) victim = k;
+        if (!c->ucache[w][j].base && k < 0) k = j;
     }
-    if (c->ucache[w][victim].base) {
-        fdev_trace_unregion(c->dev, c->ucache[w][victim].base);
-        fdev_unimport(c->dev, c->ucache[w][victim].base);
+    if (!s->unew || k < 0) {
+        /* the exporter holds an entry this cache lacks (never expected: both apply one rule
+         * to one sequence): make room, and report it */
+        fprintf(stderr, "ftar: rank %d: call %d: rank %d's allocation %llu is not in this rank's cache (%s)\n", c->wrank,
+                c->ncalls, w, (unsigned long long)id, s->unew ? "full" : "exported earlier");
+        if (k < 0) {
+            k = 0;
+            for (int j = 1; j < FTAR_UCACHE; j++)
+                if (c->ucache[w][j].last < c->ucache[w][k].last) k = j;
+            drop_mapping(c, w, k);
+        }
     }
-    c->ucache[w][victim].base = NULL;
-    c->ucache[w][victim].id = 0;
     void *base = NULL;
     if (fdev_import(c->dev, s->uhandle, &base)) {
+        fprintf(stderr, "ftar: rank %d: call %d: mapping rank %d's allocation %llu failed: %s\n", c->wrank, c->ncalls, w,
+                (unsigned long long)id, fdev_last_error());
         *failed = !ftar_is_dead(c, w); /* a dead rank's data is never used */
         return NULL;
     }
-    c->ucache[w][victim].id = id;
-    c->ucache[w][victim].base = base;
-    c->ucache[w][victim].used = ++c->ucache_clock;
+    if (c->verbose >= 2)
+        fprintf(stderr, "ftar[%d] call %d: mapped rank %d's allocation %llu\n", c->wrank, c->ncalls, w,
+                (unsigned long long)id);
+    c->ucache[w][k].id = id;
+    c->ucache[w][k].base = base;
+    c->ucache[w][k].last = now;
     char nm[32];
     snprintf(nm, sizeof(nm), "U%llu", (unsigned long long)id);
     fdev_trace_region(c->dev, base, s->uoff + c->in_bytes, w, nm);
     return (char *)base + s->uoff;
 }
 
-static uint64_t published_id(ftar_comm *c, int w)
-{
-    ftar_slot *s = &c->job.shm->slot[w];
-    return s->useq == (uint64_t)c->ncalls ? s->uid : 0;
-}
-
-/* Map the peers' exported inputs.  Every rank sees the same published ids, so when none
- * changed since the last call every mapping is a cache hit everywhere; otherwise some
- * rank may have to map a new allocation, and an extra agree round makes sure every rank
- * managed before anyone reads through a mapping -- if one did not, the job stops
- * exporting for good: the exporters stage their inputs in IN and the call goes on. */
+/* Map the peers' exported inputs.  A mapping is made only where an exporter published a new
+ * cache entry (unew), and every rank reads the same words: then an extra agree round makes
+ * sure every rank managed before anyone reads through a mapping -- if one did not, the job
+ * stops exporting for good: the exporters stage their inputs in IN and the call goes on.
+ * A call whose buffers the peers all hold already (any number of alternating buffers up to
+ * FTAR_UCACHE) needs no extra round. */
 void ftar_resolve_inputs(ftar_comm *c)
 {
     int changed = 0, failed = 0;
+    unsigned char member[FTAR_MAX_RANKS];
+    memset(member, 0, sizeof(member));
     for (int i = 0; i < c->size; i++) { /* every member, this rank included: uniform */
         int w = c->order[i];
-        if (published_id(c, w) != c->last_uid[w]) changed = 1;
+        const ftar_slot *s = &c->job.shm->slot[w];
+        member[w] = 1;
+        if (s->useq == (uint64_t)c->ncalls && s->uid && s->unew) changed = 1;
     }
+    /* a rank no longer in the comm: its inputs are never read again, and a mapping would keep
+     * its memory alive */
+    for (int w = 0; w < c->wsize; w++)
+        if (!member[w])
+            for (int k = 0; k < FTAR_UCACHE; k++) drop_mapping(c, w, k);
     for (int i = 0; i < c->size; i++) {
         int w = c->order[i];
         if (w != c->wrank) c->peer_in[w] = peer_sbuf(c, w, &failed);
@@ -419,10 +488,10 @@ void ftar_resolve_inputs(ftar_comm *c)
             ftar_inputs_done(c);
             (void)ftar_sync(c); /* every staged copy is ready */
         }
-    }
-    for (int i = 0; i < c->size; i++) {
-        int w = c->order[i];
-        c->last_uid[w] = c->export_user ? published_id(c, w) : 0;
+    } else if (failed) {
+        /* a mapping outside the agreed ones failed (the caches disagreed): no uniform fallback */
+        fprintf(stderr, "ftar: rank %d: cannot map a peer's send buffer: %s\n", c->wrank, fdev_last_error());
+        ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
     }
 }
 

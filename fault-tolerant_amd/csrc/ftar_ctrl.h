@@ -25,7 +25,7 @@
 #include "ftar_dev.h"
 
 #define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
-#define FTAR_SHM_VERSION 6
+#define FTAR_SHM_VERSION 7
 /* digest of the headers this binary was built from (fault-tolerant_amd/tools/build_id.sh abi,
  * passed by the Makefiles): the launcher writes it into the control block, every rank compares */
 #ifndef FTAR_ABI_ID
@@ -65,6 +65,8 @@ typedef struct {
     uint64_t uoff;                            /* sbuf's byte offset in the allocation */
     uint64_t useq;                            /* the call (1, 2, ...) these fields belong to */
     uint64_t ufail;                           /* call in which this rank failed to map a peer's */
+    uint64_t unew;                            /* 1: uid entered the peers' mapping caches with this
+                                                 publication (they map it now), 0: they hold it */
     /* exchange entry: set to seq + 1 when the rank passes an exchange step's BEFORE
      * point (the agree sequence number is uniform at every step), so a partner decides
      * "the exchange failed" only for a rank that died before entering it */

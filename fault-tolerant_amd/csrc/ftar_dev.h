@@ -75,7 +75,8 @@ int fdev_free(ftar_dev *d, void *ptr);
 int fdev_import(ftar_dev *d, const void *handle, void **ptr);
 /* Export the device allocation holding [ptr, ptr + bytes): its IPC handle, a per-process
  * unique allocation id (a freed and re-used address gets a new one) and ptr's offset in
- * it.  Nonzero if the memory cannot be shared (the caller then stages it). */
+ * it; handle NULL: the id and offset only, nothing exported.  Nonzero if the memory
+ * cannot be shared (the caller then stages it). */
 int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, uint64_t *id, size_t *offset);
 int fdev_unimport(ftar_dev *d, void *ptr);
 /* 0 if the device can access [ptr, ptr + bytes): this device's memory inside one

@@ -57,6 +57,10 @@ unsigned nt_store() { return g_nt == 0 ? 0u : 1u; }
 
 int set_err(hipError_t e, const char *what)
 {
+    // the runtime keeps the error as its "last error" until it is read: a failure handled
+    // here (a refused IPC mapping falls back to staging) must not resurface as the error of
+    // the next, unrelated launch
+    (void)hipGetLastError();
     snprintf(g_err, sizeof(g_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
     return 101; // FTAR_ERR_DEVICE
 }
@@ -138,8 +142,6 @@ int fdev_open(int device, ftar_dev **out)
     ftar_dev *d = new ftar_dev();
     d->device = device;
     d->profiling = 0;
-    memset(d->exp, 0, sizeof(d->exp));
-    d->exp_clock = 0;
     memset(&d->ctr, 0, sizeof(d->ctr));
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -359,23 +361,17 @@ int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, 
     }
     size_t off = (size_t)((const char *)ptr - (const char *)base);
     if (off + bytes > size) return 1;
-    int k = 0, victim = 0;
-    for (; k < 4 && d->exp[k].id != bid; k++)
-        if (d->exp[k].used < d->exp[victim].used) victim = k;
-    if (k == 4) {
-        hipIpcMemHandle_t h;
-        if (hipIpcGetMemHandle(&h, base) != hipSuccess) {
-            (void)hipGetLastError();
-            return 1;
-        }
-        k = victim;
-        memcpy(d->exp[k].handle, &h, FDEV_HANDLE_BYTES);
-        d->exp[k].id = bid;
-    }
-    d->exp[k].used = ++d->exp_clock;
-    memcpy(handle, d->exp[k].handle, FDEV_HANDLE_BYTES);
     *id = bid;
     *offset = off;
+    if (!handle) return 0; // identify only: no export
+    // a fresh handle per export: the comm exports an allocation only when it enters the
+    // peers' mapping caches (ftar_comm.c xcache_admit), not at every call
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, base) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    memcpy(handle, &h, FDEV_HANDLE_BYTES);
     return 0;
 }
 

@@ -61,11 +61,6 @@ struct ftar_dev {
     std::vector<fdevi::Pending> pending;
     std::vector<hipEvent_t> event_pool;
     fdev_counters ctr;
-    struct { // recently exported caller allocations (a handle per allocation id)
-        unsigned long long id, used;
-        unsigned char handle[FDEV_HANDLE_BYTES];
-    } exp[4];
-    unsigned long long exp_clock;
     int export_retries;
     // Completion signals of short launches (ftar_kernels.h KSignal): a drain
     // whose stream holds only signalled launches since the previous drain waits for the

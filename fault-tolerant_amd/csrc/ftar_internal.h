@@ -49,21 +49,31 @@ struct ftar_comm {
 
     const void *uin; /* the current call's buffers (WS_UIN / WS_UOUT) */
     void *uout;
-    /* peers' exported send buffers (mesh Raben reads them in place): a few mappings per
-     * peer, keyed by the peer's allocation id */
-#define FTAR_UCACHE 4
+    /* peers' exported send buffers (mesh Raben reads them in place): up to FTAR_UCACHE
+     * mappings per peer, keyed by the peer's allocation id.  Every rank keeps the same cache
+     * of its OWN allocations (xcache: the mirror of what each peer holds of it), so the
+     * exporter knows without a round trip whether its peers hold this call's send buffer: a
+     * hit is read in place, a miss with a free slot is exported and mapped, a miss in a full
+     * cache is staged in IN (a local copy) -- a caller cycling through more send buffers than
+     * the cache holds never closes and re-opens mappings call after call (0.4 ms per close,
+     * tools/ipc_probe.hip).  An entry unused for FTAR_UCACHE_IDLE calls leaves both caches
+     * alike (its allocation may be gone: the mapping would keep the peer's memory alive). */
+#define FTAR_UCACHE 8
+#define FTAR_UCACHE_IDLE 256
     struct {
         uint64_t id;
         void *base;
-        uint64_t used;
+        uint64_t last; /* the call that last used it */
     } ucache[FTAR_MAX_RANKS][FTAR_UCACHE];
-    uint64_t ucache_clock;
+    struct {
+        uint64_t id, last;
+    } xcache[FTAR_UCACHE];
+    uint64_t ucache_idle; /* FTAR_UCACHE_IDLE (the hooks build: FTAR_UCACHE_IDLE_CALLS) */
     /* this call's IN: the caller's exported sbuf itself (in_alias) or the staged copy;
      * peer_in[w] likewise for every peer (NULL: its staged IN) -- see ftar_buf */
     const void *in_alias;
     size_t in_bytes;
     void *peer_in[FTAR_MAX_RANKS];
-    uint64_t last_uid[FTAR_MAX_RANKS]; /* peers' published allocation ids in the last call */
     int export_user;     /* FTAR_EXPORT (default 1): let peers read sbuf in place where possible */
     size_t stage_max;    /* FTAR_STAGE_MAX bytes: inputs up to this size are staged, never read in place */
     int host_pipe;       /* FTAR_HOST_PIPE (default 1): chunk-pipelined host-buffer Raben where it applies */

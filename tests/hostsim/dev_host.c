@@ -211,6 +211,18 @@ static int drop(void *ptr, int unlink_it)
     return -1;
 }
 
+/* TEST-ONLY: "device memory" a caller owns (ftar_probe's send buffers under
+ * FTAR_PROBE_CYCLE_SEQ): a shared-memory object like the library's own, so the library can
+ * export it and its peers map it, as hipMalloc memory */
+void *ftar_hostsim_device_alloc(size_t bytes)
+{
+    void *p = NULL;
+    unsigned char h[FDEV_HANDLE_BYTES];
+    return fdev_alloc_shared(NULL, bytes ? bytes : 1, &p, h) == 0 ? p : NULL;
+}
+
+void ftar_hostsim_device_free(void *p) { (void)drop(p, 1); }
+
 int fdev_free(ftar_dev *d, void *ptr)
 {
     if (!ptr) return 0;
@@ -256,8 +268,10 @@ int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, 
     for (int i = 0; i < MAXMAP; i++) {
         const char *b = (const char *)g_map[i].p;
         if (!b || !g_map[i].own || p < b || p + bytes > b + g_map[i].n) continue;
-        memset(handle, 0, FDEV_HANDLE_BYTES);
-        snprintf((char *)handle, FDEV_HANDLE_BYTES, "%s", g_map[i].name);
+        if (handle) { /* NULL: identify only */
+            memset(handle, 0, FDEV_HANDLE_BYTES);
+            snprintf((char *)handle, FDEV_HANDLE_BYTES, "%s", g_map[i].name);
+        }
         *id = g_map[i].id;
         *offset = (size_t)(p - b);
         return 0;

@@ -15,7 +15,10 @@
  *      FTAR_PROBE_OFFSET=k (buffers start k elements past a 16-byte boundary),
  *      FTAR_PROBE_PINNED=1 (buffers from hipHostMalloc, looked up in the loaded HIP runtime:
  *      the _host entry points then run zero copy; host-sim build: no runtime, plain memory),
- *      FTAR_PROBE_SLEEP_US=t (sleep before every call: a late rank, with FTAR_PROBE_RANK_ENV)
+ *      FTAR_PROBE_SLEEP_US=t (sleep before every call: a late rank, with FTAR_PROBE_RANK_ENV),
+ *      FTAR_PROBE_CYCLE_SEQ=i,j,... (host-sim, with FTAR_PROBE_DEVICE=1: call k sends from
+ *      exportable buffer number seq[k], each holding the input -- a caller cycling its send
+ *      buffers through the peers' mapping caches)
  */
 #include <dlfcn.h>
 #include <stdio.h>
@@ -90,9 +93,29 @@ int main(void)
     fclose(f);
     void *pristine = malloc(bytes ? bytes : 1);
     memcpy(pristine, in, bytes);
+    /* FTAR_PROBE_CYCLE_SEQ: the send buffer of every call, from a set of exportable buffers */
+    int seq[256], nseq = 0, nbuf = 0;
+    char *cyc[64] = {0};
+    void *(*dev_alloc)(size_t) = NULL;
+    void (*dev_free)(void *) = NULL;
+    if (getenv("FTAR_PROBE_CYCLE_SEQ")) {
+        dev_alloc = (void *(*)(size_t))dlsym(RTLD_DEFAULT, "ftar_hostsim_device_alloc");
+        dev_free = (void (*)(void *))dlsym(RTLD_DEFAULT, "ftar_hostsim_device_free");
+        if (!dev_alloc || !dev_free) return 6;
+        for (const char *q = getenv("FTAR_PROBE_CYCLE_SEQ"); *q && nseq < 256; q += strcspn(q, ","), q += *q == ',') {
+            seq[nseq] = atoi(q);
+            if (seq[nseq] < 0 || seq[nseq] >= 64) return 6;
+            if (seq[nseq] + 1 > nbuf) nbuf = seq[nseq] + 1;
+            nseq++;
+        }
+        for (int b = 0; b < nbuf; b++) {
+            if (!(cyc[b] = dev_alloc(bytes + pad + 64))) return 5;
+            memcpy(cyc[b] + pad, in, bytes);
+        }
+    }
     for (int it = 0; it < iters; it++) {
         memset(out, 0xEE, bytes);
-        const void *src = in;
+        const void *src = nseq ? (const void *)(cyc[seq[it % nseq]] + pad) : in;
         if (inplace) {
             memcpy(out, in, bytes);
             src = out;
@@ -106,7 +129,7 @@ int main(void)
         else
             rc = rd ? ftar_recursive_doubling_host(src, out, count, (ftar_dtype)dt, (ftar_op)op, comm)
                     : ftar_allreduce_rabenseifner_host(src, out, count, (ftar_dtype)dt, (ftar_op)op, comm);
-        if (!inplace && memcmp(in, pristine, bytes) != 0) rc = 99; /* the send buffer was written */
+        if (!inplace && memcmp(src, pristine, bytes) != 0) rc = 99; /* the send buffer was written */
         int crank = -1, csize = -1;
         ftar_comm_rank(comm, &crank);
         ftar_comm_size(comm, &csize);
@@ -125,6 +148,7 @@ int main(void)
         fclose(f);
     }
     ftar_finalize(comm);
+    for (int b = 0; b < nbuf; b++) dev_free(cyc[b]);
     free(pristine);
     probe_free(in_mem, pinned);
     probe_free(out_mem, pinned);

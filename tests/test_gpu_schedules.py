@@ -463,6 +463,27 @@ def test_mesh_sbuf_reallocated(oracle, p):
         assert np.array_equal(r.outputs[w][1].view(np.uint32), (-o.outputs[w]).view(np.uint32))
 
 
+@pytest.mark.parametrize("p,k", [(4, 9), (2, 5)])
+def test_send_buffer_cycling(tmp_path, p, k):
+    """A caller cycling its send buffer through more allocations than the peers' mapping
+    cache holds (FTAR_UCACHE = 8; a bucketed all-reduce): every result exact, no mapping
+    closed and re-opened per call (round 6 found such churn refused with 'invalid device
+    pointer' at 4 ranks, and 8x slower calls at 2), the buffers beyond the cache staged."""
+    import subprocess
+    import sys
+    env = dict(os.environ, FTAR_PROBE_DIR=str(tmp_path), FTAR_CYCLE_BUFFERS=str(k))
+    cmd = [os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ALL_ON_GPU0, sys.executable, "-u",
+           os.path.join(H.ROOT, "tests", "cycle_worker.py")]
+    cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    assert "mapping rank" not in cp.stderr and "not in this rank's cache" not in cp.stderr, cp.stderr[-3000:]
+    for r in range(p):
+        got = (tmp_path / f"cycle_{r}.txt").read_text()
+        assert got.startswith("ok "), (r, got, cp.stderr[-2000:])
+        # one 16 MiB call: far below the ~0.4 ms a mapping's close costs per peer
+        assert float(got.split("median_us=")[1]) < 400, got
+
+
 @pytest.mark.parametrize("p,count", [(8, (1 << 23) + 77), (2, (1 << 22) + 5)])
 def test_host_pipeline_chunks(oracle, p, count):
     """Host-buffer entry point at >= 16 MiB, power of two: chunk Allreduces with H2D and

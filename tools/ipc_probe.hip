@@ -15,6 +15,10 @@
 //       pattern in each), imports the peer's K, checks every import reads its owner's pattern,
 //       stores a word into every imported block, and each owner checks the words landed;
 //       import / close times reported at 124 and at K.
+//   reexport: one allocation exported again and again (a fresh handle per round) and
+//       imported by the peer under three disciplines -- each handle opened and closed before
+//       the next export; the first handle re-opened after its close; each new handle opened
+//       while the previous import is still open -- the error of every open.
 // Usage: ipc_probe [K blocks per process, default 252] [MiB per block, default 4]
 // Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/ipc_probe.hip -o tools/_build/ipc_probe
 #include <hip/hip_runtime.h>
@@ -231,6 +235,60 @@ static void capacity(int K, size_t s)
     fflush(stdout);
 }
 
+static void reexport()
+{
+    const size_t s = 16ull << 20;
+    void *a = nullptr;
+    if (me == 0) {
+        (void)hipMalloc(&a, s);
+        (void)hipMemsetD32((hipDeviceptr_t)a, pattern(0, 7), s / 4);
+        (void)hipDeviceSynchronize();
+    }
+    const char *names[3] = {"open_close_each", "reopen_first_after_close", "open_while_previous_open"};
+    for (int mode = 0; mode < 3; mode++) {
+        char log[1024];
+        int off = 0, bad = 0;
+        void *prev = nullptr;
+        for (int r = 0; r < 5; r++) {
+            if (me == 0 && (mode != 1 || r == 0)) {
+                if (hipIpcGetMemHandle(&S->hk[0][r], a) != hipSuccess) {
+                    (void)hipGetLastError();
+                    S->fail = 1;
+                }
+            }
+            barrier();
+            if (me == 1) {
+                void *imp = nullptr;
+                hipError_t e = hipIpcOpenMemHandle(&imp, S->hk[0][mode == 1 ? 0 : r], hipIpcMemLazyEnablePeerAccess);
+                unsigned w = 0;
+                if (e == hipSuccess) {
+                    if (hipMemcpy(&w, imp, 4, hipMemcpyDeviceToHost) != hipSuccess) (void)hipGetLastError();
+                } else {
+                    (void)hipGetLastError();
+                }
+                const bool ok = e == hipSuccess && w == pattern(0, 7);
+                bad += !ok;
+                off += snprintf(log + off, sizeof(log) - off, "%s\"%s\"", r ? ", " : "", ok ? "ok" : hipGetErrorString(e));
+                if (mode == 2) {
+                    if (prev) (void)hipIpcCloseMemHandle(prev);
+                    prev = imp;
+                } else if (imp) {
+                    (void)hipIpcCloseMemHandle(imp);
+                }
+            }
+            barrier();
+        }
+        if (me == 1) {
+            if (prev) (void)hipIpcCloseMemHandle(prev);
+            printf("{\"phase\": \"reexport\", \"mode\": \"%s\", \"bad\": %d, \"opens\": [%s]}\n", names[mode], bad, log);
+            fflush(stdout);
+        }
+        barrier();
+    }
+    if (me == 0) (void)hipFree(a);
+    barrier();
+}
+
 int main(int argc, char **argv)
 {
     int K = argc > 1 ? atoi(argv[1]) : 252;
@@ -250,6 +308,7 @@ int main(int argc, char **argv)
             importer_reuse();
             growth();
             capacity(K, mib << 20);
+            reexport();
             _exit(0);
         }
     }
