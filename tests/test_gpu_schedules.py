@@ -463,15 +463,18 @@ def test_mesh_sbuf_reallocated(oracle, p):
         assert np.array_equal(r.outputs[w][1].view(np.uint32), (-o.outputs[w]).view(np.uint32))
 
 
-@pytest.mark.parametrize("p,k", [(4, 9), (2, 5)])
-def test_send_buffer_cycling(tmp_path, p, k):
+@pytest.mark.parametrize("p,k,slices,inplace", [(4, 9, 0, 0), (2, 5, 0, 0), (4, 6, 1, 0), (4, 10, 0, 1)])
+def test_send_buffer_cycling(tmp_path, p, k, slices, inplace):
     """A caller cycling its send buffer through more allocations than the peers' mapping
     cache holds (FTAR_UCACHE = 8; a bucketed all-reduce): every result exact, no mapping
     closed and re-opened per call (round 6 found such churn refused with 'invalid device
-    pointer' at 4 ranks, and 8x slower calls at 2), the buffers beyond the cache staged."""
+    pointer' at 4 ranks, and 8x slower calls at 2), the buffers beyond the cache staged.  slices:
+    the buffers are views of one allocation at unaligned offsets (one entry, k offsets);
+    inplace: every call with the send buffer as its receive buffer."""
     import subprocess
     import sys
-    env = dict(os.environ, FTAR_PROBE_DIR=str(tmp_path), FTAR_CYCLE_BUFFERS=str(k))
+    env = dict(os.environ, FTAR_PROBE_DIR=str(tmp_path), FTAR_CYCLE_BUFFERS=str(k), FTAR_CYCLE_SLICES=str(slices),
+               FTAR_CYCLE_INPLACE=str(inplace))
     cmd = [os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ALL_ON_GPU0, sys.executable, "-u",
            os.path.join(H.ROOT, "tests", "cycle_worker.py")]
     cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
