@@ -487,6 +487,22 @@ def test_send_buffer_cycling(tmp_path, p, k, slices, inplace):
         assert float(got.split("median_us=")[1]) < 400, got
 
 
+@pytest.mark.parametrize("p", [4, 3, 8])
+def test_mixed_buckets_one_job(tmp_path, p):
+    """A training step's gradient all-reduce as the library sees it: buckets of 7 .. 6 Mi
+    elements in four dtypes, both schedules interleaved, some in place, each bucket its own
+    buffer, four steps (forward and reversed order): every result exact."""
+    import subprocess
+    import sys
+    env = dict(os.environ, FTAR_PROBE_DIR=str(tmp_path))
+    cmd = [os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ALL_ON_GPU0, sys.executable, "-u",
+           os.path.join(H.ROOT, "tests", "bucket_worker.py")]
+    cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    for r in range(p):
+        assert (tmp_path / f"bucket_{r}.txt").read_text() == "ok", (r, cp.stderr[-2000:])
+
+
 @pytest.mark.parametrize("p,count", [(8, (1 << 23) + 77), (2, (1 << 22) + 5)])
 def test_host_pipeline_chunks(oracle, p, count):
     """Host-buffer entry point at >= 16 MiB, power of two: chunk Allreduces with H2D and
