@@ -336,6 +336,14 @@ int fdev_import(ftar_dev *d, const void *handle, void **ptr)
     HIPCHK(hipSetDevice(d->device));
     hipIpcMemHandle_t h;
     memcpy(&h, handle, FDEV_HANDLE_BYTES);
+#ifdef FTAR_TEST_HOOKS
+    // TEST-ONLY (lib/libftar_hooks.so): FTAR_FAIL_IMPORT=k -- this process's k-th and later
+    // imports are refused by the runtime itself (a zeroed handle), leaving the runtime's
+    // sticky last error behind as a real refusal does (tests/test_gpu_schedules.py)
+    static int nimport;
+    const char *fi = getenv("FTAR_FAIL_IMPORT");
+    if (fi && ++nimport >= atoi(fi)) memset(&h, 0, sizeof(h));
+#endif
     HIPCHK(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
     return 0;
 }

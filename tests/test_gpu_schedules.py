@@ -487,6 +487,28 @@ def test_send_buffer_cycling(tmp_path, p, k, slices, inplace):
         assert float(got.split("median_us=")[1]) < 400, got
 
 
+def test_peer_input_map_refused_falls_back():
+    """The runtime refuses a peer send-buffer mapping (the hooks build's FTAR_FAIL_IMPORT: the
+    13th import of every rank -- after the 4 x 3 workspace mappings -- gets a zeroed handle):
+    every rank stages its input from then on, and the call and the next ones are exact.  The
+    refusal leaves the runtime's sticky error behind; before round 6 it resurfaced as the
+    fallback's next launch error and aborted the job."""
+    import json
+    import subprocess
+    env = dict(os.environ, FTAR_FAIL_IMPORT="13")
+    env.pop("FTAR_KILL", None)
+    cmd = [os.path.join(H.PKG, "bin", "ftrun"), "-np", "4", "--devmap", ALL_ON_GPU0,
+           os.path.join(H.PKG, "bin", "ftbench_hooks"), "raben", str(1 << 22), "3"]
+    cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    assert "inputs are staged from now on" in cp.stderr, cp.stderr[-2000:]
+    lines = [json.loads(x) for x in cp.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 4, cp.stdout[-2000:]
+    for ln in lines:
+        for call in ln["calls"]:
+            assert call["rc"] == 0 and call["value"] == 6.0 and call["uniform"], ln
+
+
 @pytest.mark.parametrize("p", [4, 3, 8])
 def test_mixed_buckets_one_job(tmp_path, p):
     """A training step's gradient all-reduce as the library sees it: buckets of 7 .. 6 Mi
