@@ -487,6 +487,38 @@ def test_send_buffer_cycling(tmp_path, p, k, slices, inplace):
         assert float(got.split("median_us=")[1]) < 400, got
 
 
+@pytest.mark.parametrize("p,kill", [(4, "2:1:1:3:6"), (5, "4:1:0:0:10")])
+def test_send_buffer_cycling_through_a_kill(tmp_path, p, kill):
+    """Recursive doubling with its callers cycling 9 send buffers, a rank killed in call 6 / 10
+    (mid-exchange; at p = 5 the rank outside the power of two, before its step): the survivors
+    recover and go on cycling on the shrunk comm -- the dead rank's mappings dropped, the
+    survivors' mirrored caches in agreement -- every result uniform, calls before the kill
+    summing every rank and calls after it the survivors'."""
+    import json
+    import subprocess
+    import sys
+    victim, call = int(kill.split(":")[0]), int(kill.split(":")[-1])
+    env = dict(os.environ, FTAR_KILL=kill, FTAR_PROBE_DIR=str(tmp_path))
+    cmd = [os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ALL_ON_GPU0, sys.executable, "-u",
+           os.path.join(H.ROOT, "tests", "kill_cycle_worker.py")]
+    cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    lines = [json.loads((tmp_path / f"kc_{r}.json").read_text()) for r in range(p) if (tmp_path / f"kc_{r}.json").exists()]
+    assert sorted(ln["rank"] for ln in lines) == [r for r in range(p) if r != victim], (cp.returncode, cp.stderr[-3000:])
+    assert "not in this rank's cache" not in cp.stderr and "mapping rank" not in cp.stderr, cp.stderr[-3000:]
+    for ln in lines:
+        for c, rec in enumerate(ln["calls"]):
+            i = rec["buffer"]
+            every = float(sum(r + 1 + 100 * i for r in range(p)))
+            survivors = float(sum(r + 1 + 100 * i for r in range(p) if r != victim))
+            assert rec["rc"] == 0 and rec["uniform"], (ln["rank"], c, rec)
+            if c < call:
+                assert rec["value"] == every and rec["size"] == p, (ln["rank"], c, rec)
+            elif c == call:  # the victim's input counted or not, as the oracle's rules decide
+                assert rec["value"] in (every, survivors) and rec["size"] == p - 1, (ln["rank"], c, rec)
+            else:
+                assert rec["value"] == survivors and rec["size"] == p - 1, (ln["rank"], c, rec)
+
+
 def test_peer_input_map_refused_falls_back():
     """The runtime refuses a peer send-buffer mapping (the hooks build's FTAR_FAIL_IMPORT: the
     13th import of every rank -- after the 4 x 3 workspace mappings -- gets a zeroed handle):
