@@ -519,6 +519,23 @@ def test_send_buffer_cycling_through_a_kill(tmp_path, p, kill):
                 assert rec["value"] == survivors and rec["size"] == p - 1, (ln["rank"], c, rec)
 
 
+@pytest.mark.parametrize("p,seed", [(4, 1), (3, 2), (8, 3)] + H.wide((4, 11), (5, 12), (2, 13), (6, 14)))
+def test_random_call_sequences(tmp_path, p, seed):
+    """120 calls drawn at random and alike on every rank -- schedule, dtype, every op the
+    dtype allows, ragged lengths up to 3 Mi, element offsets, in place or not, fresh or
+    re-used send buffers -- each result exact against the value every rank computes from all
+    ranks' inputs (small integers: one exact answer in every dtype)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, FTAR_PROBE_DIR=str(tmp_path), FTAR_FUZZ_SEED=str(seed))
+    cmd = [os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ALL_ON_GPU0, sys.executable, "-u",
+           os.path.join(H.ROOT, "tests", "fuzz_worker.py")]
+    cp = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
+    assert cp.returncode == 0, cp.stderr[-3000:]
+    for r in range(p):
+        assert (tmp_path / f"fuzz_{r}.txt").read_text() == "ok 120", (r, (tmp_path / f"fuzz_{r}.txt").read_text())
+
+
 def test_peer_input_map_refused_falls_back():
     """The runtime refuses a peer send-buffer mapping (the hooks build's FTAR_FAIL_IMPORT: the
     13th import of every rank -- after the 4 x 3 workspace mappings -- gets a zeroed handle):
