@@ -69,7 +69,10 @@ def main():
         algo = rng.choice(["allreduce_rabenseifner", "recursive_doubling"])
         dt, code = rng.choice(DTYPES)
         op = rng.choice(INT_OPS if code in (0, 2) else FLOAT_OPS)
-        n = rng.choice([0, 1, 2, 3, 5, 17, 255, 1000, 4099, 65536, 100003, 1 << 20, (1 << 20) + 9, 3 << 20])
+        # around every size threshold too: FTAR_STAGE_MAX / FTAR_ONESHOT_MAX / FTAR_GATE_MAX (1 MiB = 2^18
+        # 4-byte or 2^17 8-byte elements), the relay's 4 MiB windows
+        n = rng.choice([0, 1, 2, 3, 5, 17, 255, 1000, 4099, 65536, 100003, (1 << 17) - 1, 1 << 17, (1 << 17) + 1,
+                        (1 << 18) - 1, 1 << 18, (1 << 18) + 1, 1 << 20, (1 << 20) + 9, 3 << 20])
         off = rng.choice([0, 0, 1, 3, 4, 64])
         inplace = rng.random() < 0.3
         fresh = rng.random() < 0.4
