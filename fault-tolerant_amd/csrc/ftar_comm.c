@@ -1065,8 +1065,6 @@ int ftar_ensure_staging(ftar_comm *c, size_t bytes)
 
 /* ---- statistics ----------------------------------------------------------- */
 
-static double g_t0;
-
 /* One user call = one stats record and one call index (FTAR_KILL ':call'), also when the
  * host pipeline runs it as several chunk Allreduces (c->chunk_cont set for chunks 2..n):
  * their counters accumulate into the record the first chunk opened. */
@@ -1075,7 +1073,7 @@ void ftar_stats_begin(ftar_comm *c)
     if (!c->chunk_cont) {
         c->ncalls++;
         memset(&c->stats, 0, sizeof(c->stats));
-        g_t0 = now_s();
+        c->t0 = now_s();
     }
     fdev_counters_reset(c->dev);
 }
@@ -1092,7 +1090,7 @@ void ftar_stats_end(ftar_comm *c)
     c->gnext.valid = 0;
     fdev_counters k;
     fdev_counters_get(c->dev, &k);
-    c->stats.wall_s = now_s() - g_t0;
+    c->stats.wall_s = now_s() - c->t0;
     c->stats.kernel_ms += k.ms[0] + k.ms[1] + k.ms[2] + k.ms[3] + k.ms[4];
     c->stats.bg_kernel_ms += k.ms[FDEV_TAG_BG];
     c->stats.step0_kernel_ms += k.ms[FDEV_TAG_STEP0];

@@ -86,6 +86,7 @@ struct ftar_comm {
 
     int profiling;
     ftar_stats stats;
+    double t0; /* start of the current user call (ftar_stats_begin) */
     int chunk_cont; /* the host pipeline's chunks 2..n of one user call (see ftar_stats_begin) */
     int verbose;
     int overlap;         /* FTAR_OVERLAP (default 1): Raben step-0 redundancy copy on the background stream */
