@@ -241,6 +241,12 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
         free(c);
         return rc;
     }
+    /* the device-wait flags (ftar_flag): the control block's flag page, mapped for this GPU */
+    if (fdev_host_map(c->dev, (void *)c->job.shm->pwflag, sizeof(c->job.shm->pwflag), &c->pwflag_dev)) {
+        fprintf(stderr, "ftar: rank %d: flag page not mapped (%s): the mesh orders its allgather on the host\n", rank,
+                fdev_last_error());
+        c->pwflag_dev = NULL;
+    }
     const char *tp = getenv("FTAR_TRACE"); /* test instrumentation: tests/fence_check.py */
     if (tp && *tp) {
         char path[512];
@@ -523,6 +529,7 @@ int ftar_finalize(ftar_comm *c)
     fdev_free(c->dev, c->hrecv);
     fdev_free(c->dev, c->pad);
     ftar_ctrl_leave(&c->job);
+    if (c->pwflag_dev) fdev_host_unmap(c->dev, (void *)c->job.shm->pwflag);
     fdev_close(c->dev);
     ftar_ctrl_detach(&c->job);
     free(c);
@@ -841,8 +848,7 @@ int ftar_drain(ftar_comm *c)
 
 void *ftar_flag(ftar_comm *c, int w)
 {
-    if (w == c->wrank) return c->ws[WS_W] ? (char *)c->ws[WS_W] + c->ws_bytes - FDEV_FLAG_BYTES : NULL;
-    return c->peer[w][WS_W] ? (char *)c->peer[w][WS_W] + c->peer_bytes[w] - FDEV_FLAG_BYTES : NULL;
+    return c->pwflag_dev ? (char *)c->pwflag_dev + (size_t)w * sizeof(c->job.shm->pwflag[0]) : NULL;
 }
 
 int ftar_watch_peers(void *arg)
@@ -985,7 +991,6 @@ void *ftar_local(ftar_comm *c, int b)
  * round 2).  Costs the old workspace's memory for the length of the call. */
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes)
 {
-    bytes += FDEV_FLAG_BYTES; /* the peer-wait flag page at the end (ftar_flag) */
     if (bytes <= c->ws_bytes && c->ws[0]) return FTAR_SUCCESS;
     if (c->ws[0] && bytes < 2 * c->ws_bytes) bytes = 2 * c->ws_bytes; /* grow geometrically: few re-exports */
     size_t nb = (bytes + WS_ALIGN - 1) / WS_ALIGN * WS_ALIGN;

@@ -25,7 +25,7 @@
 #include "ftar_dev.h"
 
 #define FTAR_SHM_MAGIC 0x46544152u /* "FTAR" */
-#define FTAR_SHM_VERSION 7
+#define FTAR_SHM_VERSION 8
 /* digest of the headers this binary was built from (fault-tolerant_amd/tools/build_id.sh abi,
  * passed by the Makefiles): the launcher writes it into the control block, every rank compares */
 #ifndef FTAR_ABI_ID
@@ -99,6 +99,12 @@ typedef struct {
     _Atomic int launcher_pid;       /* ftrun pid when launched by it, else 0 */
     _Atomic uint64_t decision[FTAR_DECISIONS];
     ftar_slot slot[FTAR_MAX_RANKS];
+    /* the mesh's device-wait flags (fdev_peer_wait), one 64-byte line per original rank, in a
+     * page of their own: every rank's GPU maps the page (hipHostRegister), its wait kernel
+     * stores its token into its own line and polls its peers' over PCIe.  Host memory is
+     * the one place every GPU of the node reads coherently while the writer's kernel runs;
+     * a flag in the writer's HBM could be served stale from the reader's L2. */
+    _Alignas(4096) _Atomic uint64_t pwflag[FTAR_MAX_RANKS][8];
 } ftar_shm;
 
 typedef struct {

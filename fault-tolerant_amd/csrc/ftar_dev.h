@@ -78,6 +78,11 @@ int fdev_import(ftar_dev *d, const void *handle, void **ptr);
  * it; handle NULL: the id and offset only, nothing exported.  Nonzero if the memory
  * cannot be shared (the caller then stages it). */
 int fdev_export_range(ftar_dev *d, const void *ptr, size_t bytes, void *handle, uint64_t *id, size_t *offset);
+/* Map host memory [p, p + bytes) -- page-aligned, possibly shared with other processes (the
+ * control block's flag page) -- into this device's address space; *devp: the address its
+ * kernels use.  fdev_host_unmap undoes it.  Host-sim: the address itself. */
+int fdev_host_map(ftar_dev *d, void *p, size_t bytes, void **devp);
+void fdev_host_unmap(ftar_dev *d, void *p);
 int fdev_unimport(ftar_dev *d, void *ptr);
 /* 0 if the device can access [ptr, ptr + bytes): this device's memory inside one
  * allocation, pinned host memory mapped at its own address, or managed memory; nonzero
@@ -139,17 +144,16 @@ int fdev_run_gated(ftar_dev *d, int dtype, int op, const fdev_seg *segs, int nse
 int fdev_gate_open(ftar_dev *d, int skip);
 
 /* Device-side order between ranks (the mesh allgather behind the peers' reduce-scatter, with
- * no host barrier between them).  fdev_peer_wait queues, on the main stream:
- * a fenced marker (everything queued so far is released to HBM, device-wide), the store of
- * `token` into `flag` (a word of this rank's exported HBM, FDEV_FLAG_BYTES at the end of its
- * W), then a one-wavefront kernel that waits until every peer's flag holds `token`.  The NEXT
- * launch on the main stream runs behind a fenced marker (the peers' data read fresh) and only
- * if that wait succeeded: when the host gives it up (fdev_peer_wait_abort: a peer died), or it
- * times out (FTAR_GATE_TIMEOUT_MS), its workgroups return untouched, and after the drain
+ * no host barrier between them).  fdev_peer_wait queues, on the main stream: a
+ * fenced marker (everything queued so far released to HBM device-wide, this GPU's caches
+ * invalidated), then a one-wavefront kernel that stores `token` into `flag` -- this rank's
+ * line of the job's flag page, host memory every rank's GPU maps (fdev_host_map) -- and waits
+ * until every peer's flag holds `token`.  The NEXT launch on the main stream runs only if that
+ * wait succeeded: when the host gives it up (fdev_peer_wait_abort: a peer died), or it times
+ * out (FTAR_GATE_TIMEOUT_MS), its workgroups return untouched, and after the drain
  * fdev_peer_wait_verdict returns 0.  Host-sim: the wait spins on the host, calling `poll`
  * (which may call fdev_peer_wait_abort); the GPU build ignores poll (the drain's poll does
  * that).  Tokens only grow: a flag holding a later token satisfies an earlier wait. */
-#define FDEV_FLAG_BYTES 4096
 #define FDEV_MAX_PEERS 15
 int fdev_peer_wait(ftar_dev *d, void *flag, void *const *peer_flags, int npeers, uint64_t token,
                    int (*poll)(void *), void *arg);

@@ -295,12 +295,6 @@ int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
             memcpy(handle, &h, FDEV_HANDLE_BYTES);
             *ptr = p;
             if (held) (void)hipFree(held);
-            // the last FDEV_FLAG_BYTES start zeroed: the peer-wait flag of a W buffer never
-            // holds a token before its owner publishes one (fdev_peer_wait)
-            if (bytes >= FDEV_FLAG_BYTES) {
-                HIPCHK(hipMemsetAsync((char *)p + bytes - FDEV_FLAG_BYTES, 0, FDEV_FLAG_BYTES, d->stream));
-                HIPCHK(hipStreamSynchronize(d->stream));
-            }
             return 0;
         }
         (void)hipGetLastError();
@@ -315,6 +309,26 @@ int fdev_alloc_shared(ftar_dev *d, size_t bytes, void **ptr, void *handle)
 }
 
 int fdev_export_retries(const ftar_dev *d) { return d->export_retries; }
+
+int fdev_host_map(ftar_dev *d, void *p, size_t bytes, void **devp)
+{
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    void *dp = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&dp, p, 0);
+    if (e != hipSuccess || !dp) {
+        (void)hipHostUnregister(p);
+        return set_err(e != hipSuccess ? e : hipErrorInvalidValue, "hipHostGetDevicePointer");
+    }
+    *devp = dp;
+    return 0;
+}
+
+void fdev_host_unmap(ftar_dev *d, void *p)
+{
+    (void)hipSetDevice(d->device);
+    if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+}
 
 int fdev_alloc_plain(ftar_dev *d, size_t bytes, void **ptr)
 {

@@ -128,8 +128,8 @@ int run_on(ftar_dev *d, hipStream_t st, int dtype, int op, const fdev_seg *segs,
     if (behind_wait) {
         // behind a peer wait: the wait's verdict decides.  No acquire of its own: the fenced
         // marker in front of the flag (fdev_peer_wait) invalidated this GPU's caches after
-        // everything this rank read before, and since then only the wait kernel has read peer
-        // memory (the flag words, a page of their own) -- no line of what this launch reads can
+        // everything this rank read before, and since then only the wait kernel has read
+        // anything (the flag words, in host memory) -- no line of what this launch reads can
         // be stale (tests/fence_check.py's acquire rule checks exactly that on the logs)
         L.sig.vword = d->gate_dw + 48;
         L.sig.vval = d->pw_vval;

@@ -87,6 +87,7 @@ struct ftar_comm {
     int profiling;
     ftar_stats stats;
     double t0; /* start of the current user call (ftar_stats_begin) */
+    void *pwflag_dev; /* the control block's flag page as this rank's GPU maps it (fdev_host_map) */
     int chunk_cont; /* the host pipeline's chunks 2..n of one user call (see ftar_stats_begin) */
     int verbose;
     int overlap;         /* FTAR_OVERLAP (default 1): Raben step-0 redundancy copy on the background stream */
@@ -128,10 +129,10 @@ int ftar_comm_rank_of(const ftar_comm *c, int w);
 
 /* collective: grow the _host entry points' staging to `bytes` (aborts the job on failure) */
 int ftar_ensure_staging(ftar_comm *c, size_t bytes);
-/* collective: grow the exported workspace to hold `bytes` per buffer (plus the peer-wait flag
- * page, FDEV_FLAG_BYTES at the end of each buffer) */
+/* collective: grow the exported workspace to hold `bytes` per buffer */
 int ftar_ensure_workspace(ftar_comm *c, size_t bytes);
-/* the peer-wait flag of original rank w: the last FDEV_FLAG_BYTES of its W (NULL: not mapped) */
+/* the device-wait flag of original rank w: its line of the control block's flag page, as this
+ * rank's GPU addresses it (NULL: the page is not mapped, the mesh orders on the host) */
 void *ftar_flag(ftar_comm *c, int w);
 /* fdev_sync's poll while a launch waits on the device for the peers (fdev_peer_wait): the
  * failure detector, and a dead member gives the wait up (fdev_peer_wait_abort) */

@@ -68,9 +68,10 @@ struct KSignal {
 };
 
 // The wait of the mesh allgather for the peers' reduce-scatter (fdev_peer_wait): ONE
-// wavefront.  Lane 0 first publishes this rank's flag (`token` into *own, system scope, then
-// written back: the tree's data was released to HBM device-wide by the fenced marker in front
-// of this kernel); then lane i polls peer i's flag over xGMI (system-scope loads, uncached)
+// wavefront.  Lane 0 first publishes this rank's flag (`token` into *own, system scope: the
+// flags are lines of one host page every rank's GPU maps, read coherently by every GPU of the
+// node; the tree's data was released to HBM device-wide by the fenced marker in front of this
+// kernel); then lane i polls peer i's flag over PCIe (system-scope loads of host memory)
 // until every one holds at least `token`, the host's abort word holds vval (a peer died: give
 // up), or `ticks` of the wall clock pass (give up, so the grid always drains).  The verdict
 // (vval = go, vval | 1 = given up) goes to *verdict_dev for the launch behind it and to the

@@ -630,7 +630,7 @@ __global__ __launch_bounds__(64) void peer_wait_kernel(PeerWait W)
     const int lane = threadIdx.x;
     if (lane == 0) {
         __hip_atomic_store(W.own, W.token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // system scope: the flag's line to HBM for the peers
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // system scope: the flag out to host memory for the peers
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     const unsigned long long *mine = lane < W.npeers ? W.peer[lane] : nullptr;

@@ -532,6 +532,8 @@ static int rb_mesh_devwait(rb_ctx *x, void *rbuf, double lb0)
     void *pf[FDEV_MAX_PEERS];
     int np = 0;
     for (int j = 1; j < p; j++) pf[np++] = ftar_flag(c, c->order[rb_real(x, v ^ j)]);
+    for (int i = 0; i < c->size; i++) /* FTAR_TRACE: each flag line is its owner's */
+        fdev_trace_region(c->dev, ftar_flag(c, c->order[i]), sizeof(c->job.shm->pwflag[0]), c->order[i], "PF");
     if (fdev_peer_wait(c->dev, ftar_flag(c, c->wrank), pf, np, token, ftar_watch_peers, c)) {
         fprintf(stderr, "ftar: rank %d: peer wait failed: %s\n", c->wrank, fdev_last_error());
         ftar_ctrl_abort(&c->job, FTAR_ERR_DEVICE);
@@ -838,7 +840,7 @@ int ftar_allreduce_rabenseifner(const void *sbuf, void *rbuf, size_t count, ftar
      * with FTAR_OPT_FLAG_SYNC off, the conservative mode of fenced-marker drains only (whose
      * pinned flag words the wait also uses) */
     x->devwait = x->mesh && !x->oneshot && !x->push && c->mesh_wait && count >= (size_t)c->size &&
-                 c->size - 1 <= FDEV_MAX_PEERS && fdev_get_knob(c->dev, FDEV_KNOB_FLAG_SYNC) == 1;
+                 c->size - 1 <= FDEV_MAX_PEERS && fdev_get_knob(c->dev, FDEV_KNOB_FLAG_SYNC) == 1 && ftar_flag(c, c->wrank);
     c->uin = sbuf;
     c->uout = rbuf;
     ftar_stats_begin(c);

@@ -211,6 +211,14 @@ static int drop(void *ptr, int unlink_it)
     return -1;
 }
 
+int fdev_host_map(ftar_dev *d, void *p, size_t bytes, void **devp)
+{
+    *devp = p; /* host memory is this layer's device memory */
+    return 0;
+}
+
+void fdev_host_unmap(ftar_dev *d, void *p) {}
+
 /* TEST-ONLY: "device memory" a caller owns (ftar_probe's send buffers under
  * FTAR_PROBE_CYCLE_SEQ): a shared-memory object like the library's own, so the library can
  * export it and its peers map it, as hipMalloc memory */
