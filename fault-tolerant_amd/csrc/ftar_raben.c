@@ -500,18 +500,19 @@ static int rb_mesh_ag_segs(rb_ctx *x, void *rbuf, fdev_seg *segs)
  * owner's block is final" -- with no idle rank every failure aborts the job at whichever
  * agree sees it (new_entry = -1, raben/errhandler.c:207-211, 377-378) -- so that fact moves
  * to the device: each rank releases its tree (a fenced marker) and publishes the call's token
- * in a flag of its own HBM; the allgather, queued right behind, runs once every peer's flag
- * holds the token.  Per call this saves one host agree round, one drain and the allgather's
- * launch latency; the call keeps its first and last agree.  A peer that dies before
- * publishing: the drain's failure detector gives the wait up (the allgather returns
- * untouched), and the last agree sees the death -- the handler aborts, as at the agree this
- * form leaves out.  A wait the device gave up with every member alive (its timeout): each
- * rank publishes its verdict in the last agree round, so all of them learn it alike; by then
- * every tree is released (each rank drained its own before arriving), the ranks whose
- * allgather returned untouched launch it again (it never writes what it reads), and one more
- * round keeps the peers' next call off their W until it is done.  Every step's kill points are passed, in the order both
- * launches are queued: RS BEFORE, DURING; AG BEFORE, DURING; then, once drained, RS AFTER /
- * BARRIER and AG AFTER / BARRIER. */
+ * in its line of the control block's flag page (host memory every GPU maps); the allgather,
+ * queued right behind, runs once every peer's flag holds the token.  Per call this saves one
+ * host agree round, one drain and the allgather's launch latency; the call keeps its first
+ * and last agree.  A peer that dies before publishing: the drain's failure detector gives
+ * the wait up (the allgather returns untouched), and the last agree sees the death -- the
+ * handler aborts, as at the agree this form leaves out.  A wait the device gave up with
+ * every member alive (its timeout): each rank publishes its verdict in the last agree round,
+ * so all of them learn it alike; by then every tree is released (each rank drained its own
+ * before arriving), the ranks whose allgather returned untouched launch it again (it never
+ * writes what it reads), and one more round keeps the peers' next call off their W until it
+ * is done.  Every step's kill points are passed, in the order both launches are queued: RS
+ * BEFORE, DURING; AG BEFORE, DURING; then, once drained, RS AFTER / BARRIER and AG AFTER /
+ * BARRIER. */
 static int rb_mesh_devwait(rb_ctx *x, void *rbuf, double lb0)
 {
     ftar_comm *c = x->c;
