@@ -536,6 +536,66 @@ def test_random_call_sequences(tmp_path, p, seed):
         assert (tmp_path / f"fuzz_{r}.txt").read_text() == "ok 120", (r, (tmp_path / f"fuzz_{r}.txt").read_text())
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3] + H.wide(4, 5, 6, 7, 8, 9))
+def test_external_kill_while_cycling(tmp_path, seed):
+    """A rank SIGKILLed from outside at a random instant of a 3000-call recursive-doubling
+    loop (4 ranks cycling 9 device send buffers): the job either recovers -- every survivor's
+    every result uniform, the full sum before the death, the survivors' sum after the comm
+    shrank -- or ends in a clean MPI_Abort (the reference's rules abort a death in RD's first
+    step); it never hangs and never returns a wrong value."""
+    import random
+    import signal
+    import subprocess
+    import sys
+    import time
+    rng = random.Random(seed)
+    p = 4
+    env = dict(os.environ, FTAR_PROBE_DIR=str(tmp_path))
+    env.pop("FTAR_KILL", None)
+    cmd = [os.path.join(H.PKG, "bin", "ftrun"), "-np", str(p), "--devmap", ALL_ON_GPU0, sys.executable, "-u",
+           os.path.join(H.ROOT, "tests", "ext_kill_worker.py")]
+    job = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        t0 = time.time()
+        while not all((tmp_path / f"ready_{r}").exists() for r in range(p)):
+            assert time.time() - t0 < 120 and job.poll() is None, "the job did not start"
+            time.sleep(0.02)
+        time.sleep(rng.uniform(0.0, 0.4))
+        victim = rng.randrange(p)
+        pids = subprocess.run(["pgrep", "-P", str(job.pid)], capture_output=True, text=True).stdout.split()
+        ranks = {}
+        for pid in pids:
+            with open(f"/proc/{pid}/environ", "rb") as f:
+                kv = dict(x.split(b"=", 1) for x in f.read().split(b"\0") if b"=" in x)
+            ranks[int(kv[b"FTAR_RANK"])] = int(pid)
+        os.kill(ranks[victim], signal.SIGKILL)
+        out, err = job.communicate(timeout=180)
+    finally:
+        if job.poll() is None:
+            job.kill()
+    aborted = "MPI_ABORT" in err
+    every = lambda i: float(sum(r + 1 + 100 * i for r in range(p)))
+    surv = lambda i: float(sum(r + 1 + 100 * i for r in range(p) if r != victim))
+    for r in range(p):
+        if r == victim:
+            continue
+        lines = (tmp_path / f"xk_{r}.txt").read_text().split()
+        recs = [lines[j:j + 6] for j in range(0, len(lines) - len(lines) % 6, 6)]
+        shrunk = False
+        for c, i, rc, size, v, uni in recs:
+            i, rc, size, v = int(i), int(rc), int(size), float(v)
+            assert rc == 0 and uni == "1", (r, c, rc, uni, err[-1500:])
+            if size < p:
+                assert v in (every(i), surv(i)) if not shrunk else v == surv(i), (r, c, v)
+                shrunk = True
+            else:
+                assert v == every(i), (r, c, v)
+        if not aborted:
+            assert len(recs) == 3000 and shrunk, (r, len(recs), err[-1500:])
+    assert aborted or job.returncode == 0, err[-2000:]
+    print(f"external kill of rank {victim}: {'aborted (MPI_Abort)' if aborted else 'recovered'}")
+
+
 def test_peer_input_map_refused_falls_back():
     """The runtime refuses a peer send-buffer mapping (the hooks build's FTAR_FAIL_IMPORT: the
     13th import of every rank -- after the 4 x 3 workspace mappings -- gets a zeroed handle):
