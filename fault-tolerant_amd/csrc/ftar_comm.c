@@ -716,16 +716,32 @@ void ftar_sync_fatal(ftar_comm *c)
     }
 }
 
+static void stale_publication(ftar_comm *c, int w, uint64_t s, uint64_t u) __attribute__((noreturn));
+static void stale_publication(ftar_comm *c, int w, uint64_t s, uint64_t u)
+{
+    fprintf(stderr, "ftar: rank %d: stale publication of rank %d (round %llu, tag %llu)\n", c->wrank, w,
+            (unsigned long long)s, (unsigned long long)(u >> 16));
+    ftar_ctrl_abort(&c->job, FTAR_ERR_STATE);
+}
+
 int64_t ftar_peer_pub(ftar_comm *c, int w)
 {
     uint64_t s = c->job.seq;
     uint64_t v = atomic_load_explicit(&c->job.shm->slot[w].pubv[s % 2], memory_order_acquire);
-    if ((v >> 16) != s) {
-        fprintf(stderr, "ftar: rank %d: stale publication of rank %d (round %llu, tag %llu)\n", c->wrank, w,
-                (unsigned long long)s, (unsigned long long)(v >> 16));
-        ftar_ctrl_abort(&c->job, FTAR_ERR_STATE);
-    }
+    if ((v >> 16) != s) stale_publication(c, w, s, v);
     return (int64_t)(v & 0xffff);
+}
+
+int ftar_peer_pub_try(ftar_comm *c, int w, int64_t *v)
+{
+    uint64_t s = c->job.seq;
+    uint64_t u = atomic_load_explicit(&c->job.shm->slot[w].pubv[s % 2], memory_order_acquire);
+    if ((u >> 16) == s) {
+        *v = (int64_t)(u & 0xffff);
+        return 1;
+    }
+    if (ftar_is_dead(c, w)) return 0; /* died before arriving: no entry for this round */
+    stale_publication(c, w, s, u);     /* a live member's entry is always there */
 }
 
 int ftar_is_dead(ftar_comm *c, int w) { return ftar_ctrl_is_dead(&c->job, w); }

@@ -162,6 +162,8 @@ uint64_t ftar_sync(ftar_comm *c);
 uint64_t ftar_step_sync(ftar_comm *c, int nsteps);
 /* value original rank w published before the last completed sync */
 int64_t ftar_peer_pub(ftar_comm *c, int w);
+/* the same, or 0 (no *v) for a rank that died before publishing it */
+int ftar_peer_pub_try(ftar_comm *c, int w, int64_t *v);
 /* agree outside the tolerant region: any new failure aborts the job */
 void ftar_sync_fatal(ftar_comm *c);
 /* drain the device stream (busy wait, abort-aware) */

@@ -54,6 +54,16 @@ static void publish_cur(rd_ctx *x) { x->c->pubval = x->cur; }
 
 static int peer_cur(rd_ctx *x, int w) { return (int)ftar_peer_pub(x->c, w); }
 
+/* A pull's source buffer when planning a step: a rank that died before the last agree left no
+ * entry for it -- its death surfaces at the step's own agree and reaches the handler there, as
+ * the reference's first Sendrecv with it would (rd/recursive_doubling.c:35-56); the pull from
+ * it is never made (its partner skips the exchange), so any buffer will do. */
+static int peer_cur_plan(rd_ctx *x, int w)
+{
+    int64_t v;
+    return ftar_peer_pub_try(x->c, w, &v) ? (int)v : x->cur;
+}
+
 static void run1(rd_ctx *x, int kind, void *out, const void *a, const void *b, int remote, int tag)
 {
     fdev_seg s = {kind, remote, out, a, b, x->count, NULL};
@@ -77,7 +87,7 @@ static int rd_plan(rd_ctx *x, int distance, int cur, int pred, ftar_plan *P)
         int cr = ftar_comm_rank_of(c, x->active[a]);
         int pw = x->active[a ^ distance];
         ftar_pull *pl = &P->pull[cr][0];
-        *pl = (ftar_pull){FDEV_REDUCE, last, pw, pred >= 0 ? pred : peer_cur(x, pw), 0, 0, 0, (int64_t)x->count, 0};
+        *pl = (ftar_pull){FDEV_REDUCE, last, pw, pred >= 0 ? pred : peer_cur_plan(x, pw), 0, 0, 0, (int64_t)x->count, 0};
         if (a == i) {
             pl->dst_buf = out;
             pl->x_buf = cur;

@@ -181,6 +181,13 @@ static int kill_point(const sim_t *s, int w, int phase, int step)
     return -1;
 }
 
+/* A failure in a region under MPI_ERRORS_ARE_FATAL (pre-step, post-step, the fatal barriers):
+ * OpenMPI's fatal handler aborts the job with the failure's error class, MPIX_ERR_PROC_FAILED
+ * (75; rd/recursive_doubling.c:56 hard-codes the same value for its own abort).  The handlers'
+ * explicit aborts keep their codes: MPI_Abort(comm, 1) (raben/errhandler.c:38,211,322,378) and
+ * 16 (rd/util.c:75). */
+#define FATAL_CODE 75
+
 static void do_abort(sim_t *s, int code)
 {
     s->aborted = 1;
@@ -462,7 +469,7 @@ int ftar_oracle_rabenseifner(int p, size_t count, int dtype, int op, const void 
              * ERRORS_ARE_FATAL barrier at :166 aborts the job */
             B.rk[w].alive = 0;
             res->status[w] = FTAR_ORACLE_DEAD;
-            do_abort(&S, 1);
+            do_abort(&S, FATAL_CODE);
         }
     if (!S.aborted) {
         size_t lh = count / 2, rh = count - count / 2;
@@ -592,7 +599,7 @@ int ftar_oracle_rabenseifner(int p, size_t count, int dtype, int op, const void 
             if (kill_point(&S, w, FTAR_PH_POST, 0) >= 0) {
                 B.rk[w].alive = 0;
                 res->status[w] = FTAR_ORACLE_DEAD;
-                do_abort(&S, 1);
+                do_abort(&S, FATAL_CODE);
             }
         }
     }
@@ -808,7 +815,7 @@ int ftar_oracle_recursive_doubling(int p, size_t count, int dtype, int op, const
             int involved = (w >= pp) || (w < B.ninactive);
             B.rk[w].alive = 0;
             res->status[w] = FTAR_ORACLE_DEAD;
-            if (involved) do_abort(&S, 1); /* Send/Recv under ERRORS_ARE_FATAL */
+            if (involved) do_abort(&S, FATAL_CODE); /* Send/Recv under ERRORS_ARE_FATAL */
             else pre_dead[npre++] = w;     /* surfaces at the first step's barrier */
         }
     if (!S.aborted) {
@@ -869,7 +876,7 @@ int ftar_oracle_recursive_doubling(int p, size_t count, int dtype, int op, const
             if (B.rk[w].alive && kill_point(&S, w, FTAR_PH_POST, 0) >= 0) {
                 B.rk[w].alive = 0;
                 res->status[w] = FTAR_ORACLE_DEAD;
-                do_abort(&S, 1);
+                do_abort(&S, FATAL_CODE);
             }
     }
     if (!S.aborted && B.nactive == 1 && p == 1) {

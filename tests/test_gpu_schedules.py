@@ -593,7 +593,11 @@ def test_external_kill_while_cycling(tmp_path, seed):
         if not aborted:
             assert len(recs) == 3000 and shrunk, (r, len(recs), err[-1500:])
     assert aborted or job.returncode == 0, err[-2000:]
-    print(f"external kill of rank {victim}: {'aborted (MPI_Abort)' if aborted else 'recovered'}")
+    import re
+    code = re.search(r"errorcode (\d+)", err)
+    why = re.findall(r"ftar: rank \d+: [^\n]*", err)[:1]
+    print(f"external kill of rank {victim}: " + (f"aborted (errorcode {code.group(1) if code else '?'}; {why})" if aborted
+                                                 else "recovered"))
 
 
 def test_peer_input_map_refused_falls_back():
