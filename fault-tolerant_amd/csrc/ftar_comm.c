@@ -214,11 +214,6 @@ int ftar_init_rank(ftar_comm **out, const char *job, int rank, int size, int dev
     c->stage_max = (size_t)v[14];
     c->host_pipe = (int)v[15];
     c->relay_min = (size_t)v[16];
-    c->ucache_idle = FTAR_UCACHE_IDLE;
-#ifdef FTAR_TEST_HOOKS
-    /* TEST-ONLY: a short idle limit, so a test reaches the send-buffer caches' evictions */
-    if (getenv("FTAR_UCACHE_IDLE_CALLS")) c->ucache_idle = (uint64_t)atoll(getenv("FTAR_UCACHE_IDLE_CALLS"));
-#endif
     int create = getenv("FTAR_LAUNCHER") == NULL;
     int rc = ftar_ctrl_attach(&c->job, job, rank, size, create);
     if (rc) {
@@ -327,17 +322,14 @@ static void release_user_peers(ftar_comm *c)
         for (int k = 0; k < FTAR_UCACHE; k++) drop_mapping(c, w, k);
 }
 
-/* The exporter's side of the send-buffer caches (ftar_internal.h): entries idle for
- * FTAR_UCACHE_IDLE calls leave first, then this call's allocation is a hit (1), enters a
- * free entry (1, *fresh: the peers map it now), or finds the cache full (0: staged).  The
- * peers' peer_sbuf applies the same rule to the same sequence of ids, so its cache of this
- * rank holds exactly these ids. */
+/* The exporter's side of the send-buffer caches (ftar_internal.h): this call's allocation is
+ * a hit (1), enters a free entry (1, *fresh: the peers map it now), or finds the cache full
+ * (0: staged).  The peers' peer_sbuf applies the same rule to the same sequence of ids, so its
+ * cache of this rank holds exactly these ids. */
 static int xcache_admit(ftar_comm *c, uint64_t id, int *fresh)
 {
     const uint64_t now = (uint64_t)c->ncalls;
     *fresh = 0;
-    for (int k = 0; k < FTAR_UCACHE; k++)
-        if (c->xcache[k].id && c->xcache[k].last + c->ucache_idle < now) c->xcache[k].id = 0;
     int free_k = -1;
     for (int k = 0; k < FTAR_UCACHE; k++) {
         if (c->xcache[k].id == id) {
@@ -403,8 +395,6 @@ static void *peer_sbuf(ftar_comm *c, int w, int *failed)
     ftar_slot *s = &c->job.shm->slot[w];
     const uint64_t id = s->uid, now = (uint64_t)c->ncalls;
     if (s->useq != now || !id) return NULL; /* staged in IN, or not published (dead) */
-    for (int k = 0; k < FTAR_UCACHE; k++)
-        if (c->ucache[w][k].base && c->ucache[w][k].last + c->ucache_idle < now) drop_mapping(c, w, k);
     int k = -1;
     for (int j = 0; j < FTAR_UCACHE; j++) {
         if (c->ucache[w][j].base && c->ucache[w][j].id == id) {

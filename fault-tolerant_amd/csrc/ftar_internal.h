@@ -56,10 +56,11 @@ struct ftar_comm {
      * hit is read in place, a miss with a free slot is exported and mapped, a miss in a full
      * cache is staged in IN (a local copy) -- a caller cycling through more send buffers than
      * the cache holds never closes and re-opens mappings call after call (0.4 ms per close,
-     * tools/ipc_probe.hip).  An entry unused for FTAR_UCACHE_IDLE calls leaves both caches
-     * alike (its allocation may be gone: the mapping would keep the peer's memory alive). */
+     * tools/ipc_probe.hip).  Entries stay until finalize (or the exporter's death): the runtime
+     * refused to re-open a mapping of an allocation this process had closed before (round 6,
+     * 4 and 8 ranks, "invalid device pointer"), so a mapping, once made, is never closed and
+     * re-made; a freed send buffer's memory stays allocated until then. */
 #define FTAR_UCACHE 8
-#define FTAR_UCACHE_IDLE 256
     struct {
         uint64_t id;
         void *base;
@@ -68,7 +69,6 @@ struct ftar_comm {
     struct {
         uint64_t id, last;
     } xcache[FTAR_UCACHE];
-    uint64_t ucache_idle; /* FTAR_UCACHE_IDLE (the hooks build: FTAR_UCACHE_IDLE_CALLS) */
     /* this call's IN: the caller's exported sbuf itself (in_alias) or the staged copy;
      * peer_in[w] likewise for every peer (NULL: its staged IN) -- see ftar_buf */
     const void *in_alias;

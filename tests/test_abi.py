@@ -163,8 +163,7 @@ def test_test_hooks_are_not_in_the_product(built):
     library does not contain them, and both export the same C ABI (VERDICT r05 next #6)."""
     hooks = os.path.join(ROOT, "fault-tolerant_amd", "lib", "libftar_hooks.so")
     prod = open(built, "rb").read()
-    for name in (b"FTAR_TRACE_DROP", b"FTAR_KILL_WITHDRAW", b"FTAR_PEER_WAIT_DELAY_US", b"FTAR_UCACHE_IDLE_CALLS",
-                 b"FTAR_FAIL_IMPORT"):
+    for name in (b"FTAR_TRACE_DROP", b"FTAR_KILL_WITHDRAW", b"FTAR_PEER_WAIT_DELAY_US", b"FTAR_FAIL_IMPORT"):
         assert name not in prod, name
         assert name in open(hooks, "rb").read(), name
     assert exported_symbols(hooks) == exported_symbols(built) == declared_functions()

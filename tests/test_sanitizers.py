@@ -79,9 +79,8 @@ def test_asan_recovery(asan_build, oracle, algo, p, kill):
 @pytest.mark.parametrize("algo,p", [("raben", 4), ("rd", 5)])
 def test_asan_send_buffer_caches(asan_build, oracle, algo, p):
     """The mirrored send-buffer caches (ftar_comm.c xcache_admit / peer_sbuf) under the
-    sanitizers: 12 exportable send buffers cycled, an idle limit of 5 calls, so entries are
-    admitted, staged, evicted and re-admitted on exporter and importers alike."""
+    sanitizers: 12 exportable send buffers cycled, so entries are admitted, hit and (beyond
+    the eighth) staged on exporter and importers alike."""
     seq = list(range(8)) + [8, 9] * 7 + list(range(12)) + [3, 2, 1, 0]
-    env = {"FTAR_PROBE_DEVICE": "1", "FTAR_PROBE_CYCLE_SEQ": ",".join(map(str, seq)), "FTAR_STAGE_MAX": "0",
-           "FTAR_UCACHE_IDLE_CALLS": "5"}
+    env = {"FTAR_PROBE_DEVICE": "1", "FTAR_PROBE_CYCLE_SEQ": ",".join(map(str, seq)), "FTAR_STAGE_MAX": "0"}
     _run(oracle, algo, oracle.random_inputs(p, 3001, seed=p + 500), env=env, iters=len(seq))
